@@ -1,0 +1,246 @@
+"""ctypes binding of libcp25.so (the C ABI declared in include/cp25.h).
+
+This module is the only place the Python host code touches native kernels. It fails loudly: if the
+library is missing or a device tensor is not on a ROCm GPU, it raises instead of falling back to a
+PyTorch/CPU implementation (there is no fallback path in the product).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libcp25.so")
+_lib: Optional[ctypes.CDLL] = None
+
+c_int64_p = ctypes.POINTER(ctypes.c_int64)
+
+
+class UniPCParams(ctypes.Structure):
+    """Mirror of `cp25_unipc_params` (include/cp25.h)."""
+
+    _fields_ = [
+        ("sigma", ctypes.c_float),
+        ("use_corr", ctypes.c_int),
+        ("order_c", ctypes.c_int),
+        ("c_a", ctypes.c_float),
+        ("c_b", ctypes.c_float),
+        ("c_c", ctypes.c_float),
+        ("c_inv_rk", ctypes.c_float),
+        ("c_rho0", ctypes.c_float),
+        ("c_rho_last", ctypes.c_float),
+        ("order_p", ctypes.c_int),
+        ("p_a", ctypes.c_float),
+        ("p_b", ctypes.c_float),
+        ("p_c", ctypes.c_float),
+        ("p_inv_rk", ctypes.c_float),
+        ("p_rho0", ctypes.c_float),
+    ]
+
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I = ctypes.c_int
+_F = ctypes.c_float
+
+# symbol -> argtypes (restype is always int)
+SIGNATURES = {
+    "cp25_attn_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, c_int64_p, _F, _P],
+    "cp25_ln_mod": [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _P, _P, _I64, _I, _I, _I64, _I64, _F, _P],
+    "cp25_final_ln_mod": [_P, _P, _P, _I64, _I64, _P, _P, _I64, _I64, _P, _I64, _I, _I, _I64, _I64, _F, _P],
+    "cp25_head_rmsnorm_rope": [_P, _I64, _I64, _I, _I, _I, _P, _P, _P, _P, _I64, _F, _P],
+    "cp25_copy_rows": [_P, _I64, _P, _I64, _I64, _I64, _P],
+    "cp25_gelu": [_P, _I64, _P],
+    "cp25_patchify": [_P, _P, _P, _P, _P, _I64, _I64, _I64, _P],
+    "cp25_cfg_velocity": [_P, _I, _P, _P, _P, _F, _I, _P, _I64, _I64, _I64, _P],
+    "cp25_unipc_step": [_P, _P, _P, _P, _P, _I64, ctypes.POINTER(UniPCParams), _P],
+    "cp25_conv3d": None,  # filled below (VAE)
+}
+
+
+def library_path() -> str:
+    return _LIB_PATH
+
+
+def load_library() -> ctypes.CDLL:
+    """Load libcp25.so (import torch first so the HIP runtime torch ships is the one bound)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        raise RuntimeError(
+            f"libcp25.so not found at {_LIB_PATH}: build it with `make -C cosmos-predict2.5_amd/csrc` "
+            "(or __graft_entry__.build()). There is no non-native fallback."
+        )
+    lib = ctypes.CDLL(_LIB_PATH)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if argtypes is None:
+                continue
+            raise RuntimeError(f"libcp25.so does not export {name}")
+        if argtypes is not None:
+            fn.argtypes = argtypes
+        fn.restype = ctypes.c_int
+    _lib = lib
+    return lib
+
+
+_ERRORS = {-22: "invalid shape/stride/pointer", -95: "unsupported dtype/size", -5: "kernel launch failed"}
+
+
+def _check(name: str, rc: int) -> None:
+    if rc != 0:
+        msg = f"{name} failed with code {rc} ({_ERRORS.get(rc, 'unknown')})"
+        if rc == -5:
+            raise RuntimeError(msg)
+        raise ValueError(msg)
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("cp25 kernels need device (HBM) tensors; got a CPU tensor")
+    return t.data_ptr()
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _i64x3(vals) -> ctypes.Array:
+    arr = (ctypes.c_int64 * 3)(*[int(v) for v in vals])
+    return arr
+
+
+# ----------------------------------------------------------------------------- attention
+def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[torch.Tensor] = None,
+             softmax_scale: Optional[float] = None) -> torch.Tensor:
+    """softmax(q k^T * scale) v for q [B, Lq, H, 128], k/v [B, Lk, H, 128] (bf16, any strides with
+    a contiguous head dim). Returns [B, Lq, H, 128] bf16."""
+    lib = load_library()
+    if q.dtype != torch.bfloat16 or k.dtype != torch.bfloat16 or v.dtype != torch.bfloat16:
+        raise ValueError("attn_fwd expects bf16 q/k/v (attention() recasts to bf16 first)")
+    B, Lq, H, D = q.shape
+    Bk, Lk, Hk, Dk = k.shape
+    if (Bk, Hk, Dk) != (B, H, D) or tuple(v.shape) != tuple(k.shape):
+        raise ValueError(f"shape mismatch q{tuple(q.shape)} k{tuple(k.shape)} v{tuple(v.shape)}")
+    for t in (q, k, v):
+        if t.stride(3) != 1:
+            raise ValueError("head dim must be contiguous")
+    if out is None:
+        out = torch.empty((B, Lq, H, D), dtype=torch.bfloat16, device=q.device)
+    scale = float(D) ** -0.5 if softmax_scale is None else float(softmax_scale)
+    rc = lib.cp25_attn_fwd(
+        _ptr(q), _ptr(k), _ptr(v), _ptr(out), B, H, Lq, Lk, D,
+        _i64x3((q.stride(0), q.stride(1), q.stride(2))),
+        _i64x3((k.stride(0), k.stride(1), k.stride(2))),
+        _i64x3((v.stride(0), v.stride(1), v.stride(2))),
+        _i64x3((out.stride(0), out.stride(1), out.stride(2))),
+        scale, _stream(q.device),
+    )
+    _check("cp25_attn_fwd", rc)
+    return out
+
+
+# ----------------------------------------------------------------------------- DiT elementwise
+def ln_mod(x: torch.Tensor, shift: torch.Tensor, scale: torch.Tensor, *, n_tok: int, B: int, tok0: int, hw: int,
+           x_st: int, x_sb: int, y: Optional[torch.Tensor] = None, gate: Optional[torch.Tensor] = None,
+           x_out: Optional[torch.Tensor] = None, h_out: Optional[torch.Tensor] = None,
+           eps: float = 1e-6) -> torch.Tensor:
+    """h = LN(x [+ gate*y]) * (1 + scale) + shift over token-major [n_tok, B, D] bf16 rows.
+    shift/scale/gate are bf16 views [B, T, D] (strides (sb, st, 1), shared by all three)."""
+    lib = load_library()
+    D = shift.shape[-1]
+    if h_out is None:
+        h_out = torch.empty((n_tok, B, D), dtype=torch.bfloat16, device=x.device)
+    if shift.stride() != scale.stride() or (gate is not None and gate.stride() != shift.stride()):
+        raise ValueError("shift/scale/gate must share strides")
+    rc = lib.cp25_ln_mod(
+        _ptr(x), x_st, x_sb, _ptr(y), _ptr(gate), _ptr(shift), _ptr(scale), shift.stride(0), shift.stride(1),
+        _ptr(x_out), _ptr(h_out), n_tok, B, D, tok0, hw, eps, _stream(x.device),
+    )
+    _check("cp25_ln_mod", rc)
+    return h_out
+
+
+def final_ln_mod(x: torch.Tensor, shift: torch.Tensor, scale: torch.Tensor, *, n_tok: int, B: int, tok0: int, hw: int,
+                 y: Optional[torch.Tensor] = None, gate: Optional[torch.Tensor] = None,
+                 eps: float = 1e-6) -> torch.Tensor:
+    lib = load_library()
+    D = shift.shape[-1]
+    out = torch.empty((n_tok, B, D), dtype=torch.float32, device=x.device)
+    gsb, gst = (gate.stride(0), gate.stride(1)) if gate is not None else (0, 0)
+    if shift.stride() != scale.stride():
+        raise ValueError("shift/scale must share strides")
+    rc = lib.cp25_final_ln_mod(
+        _ptr(x), _ptr(y), _ptr(gate), gsb, gst, _ptr(shift), _ptr(scale), shift.stride(0), shift.stride(1),
+        _ptr(out), n_tok, B, D, tok0, hw, eps, _stream(x.device),
+    )
+    _check("cp25_final_ln_mod", rc)
+    return out
+
+
+def head_rmsnorm_rope(buf: torch.Tensor, *, n_rows: int, B: int, H: int, head_off: int, weight: torch.Tensor,
+                      cos: Optional[torch.Tensor] = None, sin: Optional[torch.Tensor] = None,
+                      out2: Optional[torch.Tensor] = None, out2_stride: int = 0, eps: float = 1e-6) -> None:
+    lib = load_library()
+    rc = lib.cp25_head_rmsnorm_rope(
+        _ptr(buf), buf.stride(-2) if buf.dim() >= 2 else buf.shape[-1], n_rows, B, H, head_off, _ptr(weight),
+        _ptr(cos), _ptr(sin), _ptr(out2), out2_stride, eps, _stream(buf.device),
+    )
+    _check("cp25_head_rmsnorm_rope", rc)
+
+
+def copy_rows(src: torch.Tensor, src_stride: int, dst: torch.Tensor, dst_stride: int, n_rows: int, width: int,
+              src_offset: int = 0) -> None:
+    lib = load_library()
+    rc = lib.cp25_copy_rows(_ptr(src) + 2 * src_offset, src_stride, _ptr(dst), dst_stride, n_rows, width,
+                            _stream(src.device))
+    _check("cp25_copy_rows", rc)
+
+
+def gelu_(x: torch.Tensor) -> torch.Tensor:
+    lib = load_library()
+    if not x.is_contiguous() or x.dtype != torch.bfloat16:
+        raise ValueError("gelu_ expects a contiguous bf16 tensor")
+    _check("cp25_gelu", lib.cp25_gelu(_ptr(x), x.numel(), _stream(x.device)))
+    return x
+
+
+def patchify(xs: torch.Tensor, gt: Optional[torch.Tensor], frame_mask: torch.Tensor,
+             pad_mask: Optional[torch.Tensor], *, tok0: int, hw: int) -> torch.Tensor:
+    lib = load_library()
+    n_tok = xs.shape[0]
+    out = torch.empty((n_tok, 72), dtype=torch.bfloat16, device=xs.device)
+    rc = lib.cp25_patchify(_ptr(xs), _ptr(gt), _ptr(frame_mask), _ptr(pad_mask), _ptr(out), n_tok, tok0, hw,
+                           _stream(xs.device))
+    _check("cp25_patchify", rc)
+    return out
+
+
+def cfg_velocity(net: torch.Tensor, noise: Optional[torch.Tensor], gt: Optional[torch.Tensor],
+                 frame_mask: Optional[torch.Tensor], guidance: float, cfg_mode: int, *, tok0: int,
+                 hw: int) -> torch.Tensor:
+    lib = load_library()
+    n_tok, B, _ = net.shape
+    out = torch.empty((n_tok, 64), dtype=torch.float32, device=net.device)
+    rc = lib.cp25_cfg_velocity(_ptr(net), B, _ptr(noise), _ptr(gt), _ptr(frame_mask), float(guidance), int(cfg_mode),
+                               _ptr(out), n_tok, tok0, hw, _stream(net.device))
+    _check("cp25_cfg_velocity", rc)
+    return out
+
+
+def unipc_step(x: torch.Tensor, v: torch.Tensor, m0: torch.Tensor, m1: torch.Tensor, last: torch.Tensor,
+               params: UniPCParams) -> None:
+    lib = load_library()
+    for t in (x, v, m0, m1, last):
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != x.numel():
+            raise ValueError("unipc_step expects contiguous fp32 tensors of equal size")
+    rc = lib.cp25_unipc_step(_ptr(x), _ptr(v), _ptr(m0), _ptr(m1), _ptr(last), x.numel(), ctypes.byref(params),
+                             _stream(x.device))
+    _check("cp25_unipc_step", rc)

@@ -1,0 +1,66 @@
+"""Context-parallel helpers (token sharding over RCCL/xGMI).
+
+The reference splits the latent along T and asserts T % cp == 0
+(cosmos_predict2/_src/imaginaire/utils/context_parallel.py:26-54), so T = 31 (121 frames) cannot run
+at CP = 2/4/8 there. This build shards the flattened (t, h, w) token axis instead: rank r owns tokens
+[r*L/cp, (r+1)*L/cp), every per-token op is local, and self-attention all-gathers K/V
+(dit.MinimalV1LVGDiT.forward_tokens). These helpers are the data plumbing around that:
+split_inputs_cp / cat_outputs_cp / broadcast equivalents on the token axis.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+def cp_rank_world(group) -> tuple[int, int]:
+    if group is None:
+        return 0, 1
+    return dist.get_rank(group), dist.get_world_size(group)
+
+
+def token_range(L: int, group) -> tuple[int, int]:
+    """(tok0, n_tok) of this rank; L must divide evenly."""
+    r, w = cp_rank_world(group)
+    if L % w:
+        raise ValueError(f"{L} tokens cannot be split evenly over cp_size {w}")
+    n = L // w
+    return r * n, n
+
+
+def split_tokens(x: torch.Tensor, group, dim: int = 0) -> torch.Tensor:
+    """Local shard of a replicated token-major tensor (split_inputs_cp on the token axis)."""
+    tok0, n = token_range(x.shape[dim], group)
+    return x.narrow(dim, tok0, n).contiguous()
+
+
+def gather_tokens(x: torch.Tensor, group) -> torch.Tensor:
+    """Concatenate every rank's token shard along dim 0 (cat_outputs_cp on the token axis)."""
+    r, w = cp_rank_world(group)
+    if w == 1:
+        return x
+    out = torch.empty((w * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x.contiguous(), group=group)
+    return out
+
+
+def broadcast(x: Optional[torch.Tensor], group, src_in_group: int = 0) -> Optional[torch.Tensor]:
+    """Broadcast from the group's first rank (robust_broadcast: shape first, then data)."""
+    r, w = cp_rank_world(group)
+    if w == 1 or x is None:
+        return x
+    src = dist.get_global_rank(group, src_in_group)
+    dev = x.device
+    shape = torch.tensor(list(x.shape), dtype=torch.int64, device=dev)
+    n = torch.tensor([shape.numel()], dtype=torch.int64, device=dev)
+    dist.broadcast(n, src, group=group)
+    if r != src_in_group:
+        shape = torch.empty(int(n.item()), dtype=torch.int64, device=dev)
+    dist.broadcast(shape, src, group=group)
+    if r != src_in_group:
+        x = torch.empty(shape.tolist(), dtype=x.dtype, device=dev)
+    x = x.contiguous()
+    dist.broadcast(x, src, group=group)
+    return x

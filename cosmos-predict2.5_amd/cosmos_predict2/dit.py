@@ -1,0 +1,401 @@
+"""MiniTrainDIT / MinimalV1LVGDiT denoiser for MI355X.
+
+Same checkpoint layout and forward semantics as the reference network
+(cosmos_predict2/_src/predict2/networks/minimal_v4_dit.py:1250-1663 and minimal_v1_lvg_dit.py:22-62),
+re-designed for the sampler hot path:
+
+* token-major activations [tokens, B, D] (CFG cond/uncond as batch B = 2, batch inner), so a
+  context-parallel shard is a contiguous token range and every GEMM is one [tokens*B, K] x [K, N];
+* all non-GEMM work of a block is HIP (libcp25.so): fused gated-residual + LayerNorm + AdaLN
+  modulate, per-head RMSNorm + 3D RoPE writing bf16 q/k in place in the fused QKV buffer, flash
+  attention reading q/k/v straight out of that buffer, exact GELU; plain GEMMs go to hipBLASLt;
+* everything that is constant across the 36 sampler steps is computed once: the crossattn_proj
+  text projection, the cross-attention K/V of every block (per prompt), the RoPE cos/sin tables;
+* AdaLN modulation of all blocks in two batched fp32 GEMMs per forward (reference: fp32 autocast).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import _native as N
+from .net_config import DiTConfig
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+# ----------------------------------------------------------------------------- weights
+def state_dict_shapes(cfg: DiTConfig) -> Dict[str, Tuple[Tuple[int, ...], torch.dtype]]:
+    """The reference's `net.*` state-dict layout (module names at minimal_v4_dit.py)."""
+    D, A, Ctx = cfg.model_channels, cfg.adaln_lora_dim, cfg.crossattn_emb_channels
+    hd = cfg.head_dim
+    dim_h = hd // 6 * 2
+    dim_t = hd - 2 * dim_h
+    len_max = max(cfg.max_img_h // cfg.patch_spatial, cfg.max_img_w // cfg.patch_spatial,
+                  cfg.max_frames // cfg.patch_temporal)
+    s: Dict[str, Tuple[Tuple[int, ...], torch.dtype]] = {
+        "x_embedder.proj.1.weight": ((D, cfg.patch_features), BF16),
+        "pos_embedder.seq": ((len_max,), BF16),
+        "pos_embedder.dim_spatial_range": ((dim_h // 2,), BF16),
+        "pos_embedder.dim_temporal_range": ((dim_t // 2,), BF16),
+        "t_embedder.1.linear_1.weight": ((D, D), BF16),
+        "t_embedder.1.linear_2.weight": ((3 * D, D), BF16),
+        "t_embedding_norm.weight": ((D,), BF16),
+        "final_layer.linear.weight": ((cfg.patch_spatial ** 2 * cfg.patch_temporal * cfg.out_channels, D), BF16),
+        "final_layer.adaln_modulation.1.weight": ((A, D), BF16),
+        "final_layer.adaln_modulation.2.weight": ((2 * D, A), BF16),
+    }
+    if cfg.use_crossattn_projection:
+        s["crossattn_proj.0.weight"] = ((Ctx, cfg.crossattn_proj_in_channels), BF16)
+        s["crossattn_proj.0.bias"] = ((Ctx,), BF16)
+    for i in range(cfg.num_blocks):
+        p = f"blocks.{i}."
+        for a in ("self_attn", "cross_attn"):
+            kv_in = D if a == "self_attn" else Ctx
+            s[p + a + ".q_proj.weight"] = ((D, D), BF16)
+            s[p + a + ".k_proj.weight"] = ((D, kv_in), BF16)
+            s[p + a + ".v_proj.weight"] = ((D, kv_in), BF16)
+            s[p + a + ".output_proj.weight"] = ((D, D), BF16)
+            s[p + a + ".q_norm.weight"] = ((hd,), BF16)
+            s[p + a + ".k_norm.weight"] = ((hd,), BF16)
+        s[p + "mlp.layer1.weight"] = ((cfg.mlp_hidden, D), BF16)
+        s[p + "mlp.layer2.weight"] = ((D, cfg.mlp_hidden), BF16)
+        for m in ("self_attn", "cross_attn", "mlp"):
+            s[p + f"adaln_modulation_{m}.1.weight"] = ((A, D), BF16)
+            s[p + f"adaln_modulation_{m}.2.weight"] = ((3 * D, A), BF16)
+    return s
+
+
+def init_state_dict(cfg: DiTConfig, seed: int = 0, device="cpu", zero_adaln_out: bool = True) -> Dict[str, torch.Tensor]:
+    """Seeded synthetic weights with the reference's init_weights distributions
+    (minimal_v4_dit.py:239-247, 386-398, 769-774, 887-889, 954-963, 1100-1122, 1445-1459).
+    zero_adaln_out=False fills the zero-initialised AdaLN output layers too (exercises the path)."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    out: Dict[str, torch.Tensor] = {}
+
+    def tn(shape, std):
+        t = torch.empty(shape, dtype=F32, device=device)
+        torch.nn.init.trunc_normal_(t, std=std, a=-3 * std, b=3 * std, generator=g)
+        return t.to(BF16)
+
+    D = cfg.model_channels
+    for name, (shape, _) in state_dict_shapes(cfg).items():
+        if name.endswith("norm.weight"):
+            out[name] = torch.ones(shape, dtype=BF16, device=device)
+        elif name == "pos_embedder.seq":
+            out[name] = torch.arange(shape[0], device=device).float().to(BF16)
+        elif name.startswith("pos_embedder.dim_"):
+            full = 2 * shape[0] if "spatial" in name else 2 * shape[0]
+            out[name] = (torch.arange(0, full, 2, device=device)[: shape[0]].float() / full).to(BF16)
+        elif name.startswith("crossattn_proj"):
+            bound = 1.0 / math.sqrt(cfg.crossattn_proj_in_channels)
+            out[name] = (torch.rand(shape, generator=g, device=device) * 2 - 1).mul_(bound).to(BF16)
+        elif name.endswith(".2.weight") and "adaln_modulation" in name and zero_adaln_out:
+            out[name] = torch.zeros(shape, dtype=BF16, device=device)
+        else:
+            fan_in = shape[1]
+            out[name] = tn(shape, 1.0 / math.sqrt(fan_in if "output_proj" not in name else D))
+    return out
+
+
+# ----------------------------------------------------------------------------- RoPE
+def rope_freqs(cfg: DiTConfig, T: int, H: int, W: int, sd: Dict[str, torch.Tensor], device) -> torch.Tensor:
+    """VideoRopePosition3DEmb.generate_embeddings (minimal_v4_dit.py:598-663) with the bf16 range
+    buffers of the checkpoint (F8): -> [T*H*W, head_dim] fp32."""
+    hd = cfg.head_dim
+    dim_h = hd // 6 * 2
+    dim_t = hd - 2 * dim_h
+    seq = sd["pos_embedder.seq"].to(device)
+    rs = sd["pos_embedder.dim_spatial_range"].to(device).float()
+    rt = sd["pos_embedder.dim_temporal_range"].to(device).float()
+    h_theta = 10000.0 * cfg.rope_h_extrapolation_ratio ** (dim_h / (dim_h - 2))
+    w_theta = 10000.0 * cfg.rope_w_extrapolation_ratio ** (dim_h / (dim_h - 2))
+    t_theta = 10000.0 * cfg.rope_t_extrapolation_ratio ** (dim_t / (dim_t - 2))
+    if H > cfg.max_img_h // cfg.patch_spatial or W > cfg.max_img_w // cfg.patch_spatial:
+        raise ValueError(f"latent patches ({H}, {W}) exceed the RoPE table")
+    eh = torch.outer(seq[:H], 1.0 / (h_theta ** rs))
+    ew = torch.outer(seq[:W], 1.0 / (w_theta ** rs))
+    et = torch.outer(seq[:T], 1.0 / (t_theta ** rt))
+    em = torch.cat([et[:, None, None].expand(T, H, W, -1), eh[None, :, None].expand(T, H, W, -1),
+                    ew[None, None, :].expand(T, H, W, -1)] * 2, dim=-1)
+    return em.reshape(T * H * W, hd).float()
+
+
+@dataclass
+class ContextCache:
+    """Per-prompt constants: projected text context and every block's cross-attention K/V."""
+
+    B: int
+    k: List[torch.Tensor]  # [B, Lctx, H, hd] bf16 (normed)
+    v: List[torch.Tensor]  # [B, Lctx, H, hd] bf16
+
+
+@dataclass
+class Geometry:
+    T: int   # latent frames (patches along t)
+    Hp: int  # patches along h
+    Wp: int  # patches along w
+    tok0: int = 0  # first global token of this rank's shard
+    n_tok: int = 0  # tokens on this rank
+
+    @property
+    def hw(self) -> int:
+        return self.Hp * self.Wp
+
+    @property
+    def L(self) -> int:
+        return self.T * self.Hp * self.Wp
+
+
+class MinimalV1LVGDiT:
+    """Inference-only DiT with the reference's state-dict layout; weights live in HBM as bf16."""
+
+    def __init__(self, cfg: DiTConfig, device="cuda"):
+        if cfg.head_dim != 128:
+            raise ValueError("the MI355X attention kernel is built for head_dim 128 (2B and 14B both use it)")
+        if cfg.patch_temporal != 1 or cfg.patch_spatial != 2 or cfg.out_channels != 16:
+            raise ValueError("patch (1,2,2) with 16 latent channels is the layout this build serves")
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.sd: Dict[str, torch.Tensor] = {}
+        self._rope_cache: Dict[Tuple[int, int, int], Tuple[torch.Tensor, torch.Tensor]] = {}
+        self.cp_group = None
+
+    # ---------------------------------------------------------------- loading
+    def load_state_dict(self, state_dict: Dict[str, torch.Tensor], strict: bool = True) -> None:
+        """Accepts the reference's checkpoint dict (`net.` prefix optional, `_extra_state` skipped,
+        model_loader.py:173-174; text2world_model_rectified_flow.py:775-783)."""
+        shapes = state_dict_shapes(self.cfg)
+        sd = {}
+        for k, v in state_dict.items():
+            if k.startswith("net_ema."):
+                continue
+            k2 = k[4:] if k.startswith("net.") else k
+            if k2.endswith("_extra_state"):
+                continue
+            if k2 in shapes:
+                sd[k2] = v
+        missing = [k for k in shapes if k not in sd]
+        if missing and strict:
+            raise KeyError(f"missing keys in DiT state dict: {missing[:8]}{'...' if len(missing) > 8 else ''}")
+        cfg = self.cfg
+        dev = self.device
+        self.sd = {k: v.to(device=dev, dtype=shapes[k][1]).contiguous() for k, v in sd.items()}
+        D = cfg.model_channels
+        p = self.sd
+        # fused / stacked views used by the hot path
+        self.w_qkv = [torch.cat([p[f"blocks.{i}.self_attn.{n}_proj.weight"] for n in "qkv"], 0).contiguous()
+                      for i in range(cfg.num_blocks)]
+        for i in range(cfg.num_blocks):
+            for n in "qkv":
+                del p[f"blocks.{i}.self_attn.{n}_proj.weight"]  # keep only the fused copy in HBM
+        self.w_ada1 = torch.cat([p[f"blocks.{i}.adaln_modulation_{m}.1.weight"]
+                                 for i in range(cfg.num_blocks) for m in ("self_attn", "cross_attn", "mlp")], 0).float()
+        self.w_ada2 = torch.stack([p[f"blocks.{i}.adaln_modulation_{m}.2.weight"]
+                                   for i in range(cfg.num_blocks) for m in ("self_attn", "cross_attn", "mlp")], 0).float()
+        self.w_final = p["final_layer.linear.weight"].float()
+        self._rope_cache.clear()
+        if D % 512:
+            raise ValueError("model_channels must be a multiple of 512")
+
+    def state_dict_keys(self) -> List[str]:
+        return list(state_dict_shapes(self.cfg).keys())
+
+    # ---------------------------------------------------------------- context parallel
+    def enable_context_parallel(self, process_group) -> None:
+        self.cp_group = process_group
+
+    def disable_context_parallel(self) -> None:
+        self.cp_group = None
+
+    @property
+    def is_context_parallel_enabled(self) -> bool:
+        return self.cp_group is not None
+
+    # ---------------------------------------------------------------- per-prompt constants
+    @torch.no_grad()
+    def prepare_context(self, crossattn_emb: torch.Tensor) -> ContextCache:
+        """crossattn_emb [B, Lctx, proj_in] -> per-block cross-attention K/V (normed)."""
+        cfg = self.cfg
+        p = self.sd
+        ctx = crossattn_emb.to(device=self.device, dtype=BF16)
+        if cfg.use_crossattn_projection:
+            ctx = F.linear(ctx, p["crossattn_proj.0.weight"], p["crossattn_proj.0.bias"]).contiguous()
+            N.gelu_(ctx)
+        B, Lc, _ = ctx.shape
+        H, hd = cfg.num_heads, cfg.head_dim
+        ks, vs = [], []
+        for i in range(cfg.num_blocks):
+            k = F.linear(ctx, p[f"blocks.{i}.cross_attn.k_proj.weight"]).contiguous()
+            N.head_rmsnorm_rope(k.view(B * Lc, H * hd), n_rows=B * Lc, B=1, H=H, head_off=0,
+                                weight=p[f"blocks.{i}.cross_attn.k_norm.weight"])
+            v = F.linear(ctx, p[f"blocks.{i}.cross_attn.v_proj.weight"]).contiguous()
+            ks.append(k.view(B, Lc, H, hd))
+            vs.append(v.view(B, Lc, H, hd))
+        return ContextCache(B=B, k=ks, v=vs)
+
+    def rope_tables(self, geo: Geometry) -> Tuple[torch.Tensor, torch.Tensor]:
+        key = (geo.T, geo.Hp, geo.Wp)
+        if key not in self._rope_cache:
+            fr = rope_freqs(self.cfg, geo.T, geo.Hp, geo.Wp, self.sd, self.device)[:, :64].contiguous()
+            self._rope_cache[key] = (torch.cos(fr).contiguous(), torch.sin(fr).contiguous())
+        c, s = self._rope_cache[key]
+        return c[geo.tok0: geo.tok0 + geo.n_tok], s[geo.tok0: geo.tok0 + geo.n_tok]
+
+    # ---------------------------------------------------------------- fp32 conditioning
+    @torch.no_grad()
+    def time_modulation(self, t_B_T: torch.Tensor):
+        """t (already * timestep_scale) [B, T] fp32 -> (block mods bf16 [nb, 3, B, T, 3D],
+        final shift/scale fp32 [B, T, D] each). fp32 math (use_wan_fp32_strategy)."""
+        cfg = self.cfg
+        p = self.sd
+        D = cfg.model_channels
+        B, T = t_B_T.shape
+        half = D // 2
+        expo = -math.log(10000) * torch.arange(half, dtype=F32, device=self.device)
+        expo = expo / (half - 0.0)
+        arg = t_B_T.flatten().float()[:, None] * torch.exp(expo)[None, :]
+        sincos = torch.cat([torch.cos(arg), torch.sin(arg)], dim=-1).view(B, T, D)
+        h = F.silu(F.linear(sincos, p["t_embedder.1.linear_1.weight"].float()))
+        lora = F.linear(h, p["t_embedder.1.linear_2.weight"].float())  # [B, T, 3D]
+        xf = sincos
+        emb = ((xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-6)) * p["t_embedding_norm.weight"].float())
+        se = F.silu(emb)  # [B, T, D]
+        nb3 = 3 * cfg.num_blocks
+        a1 = F.linear(se, self.w_ada1).view(B * T, nb3, -1).transpose(0, 1)  # [nb3, BT, A]
+        a2 = torch.bmm(a1, self.w_ada2.transpose(1, 2))  # [nb3, BT, 3D]
+        mods = (a2 + lora.view(1, B * T, 3 * D)).view(cfg.num_blocks, 3, B, T, 3 * D).to(BF16)
+        f1 = F.linear(se, p["final_layer.adaln_modulation.1.weight"].float())
+        f2 = F.linear(f1, p["final_layer.adaln_modulation.2.weight"].float()) + lora[..., : 2 * D]
+        shift_f, scale_f = f2.chunk(2, dim=-1)
+        return mods, shift_f, scale_f
+
+    # ---------------------------------------------------------------- hot path
+    @torch.no_grad()
+    def forward_tokens(self, patch_rows: torch.Tensor, t_B_T: torch.Tensor, ctx: ContextCache,
+                       geo: Geometry) -> torch.Tensor:
+        """patch_rows: [n_tok, Bx, 72] bf16 (Bx = 1 shares the input across the CFG batch);
+        t_B_T: [B, T] fp32, already scaled. Returns the final layer output [n_tok, B, 64] fp32
+        (feature order (p1 p2 C) = patch layout)."""
+        cfg = self.cfg
+        p = self.sd
+        B = ctx.B
+        D, H, hd = cfg.model_channels, cfg.num_heads, cfg.head_dim
+        n = geo.n_tok
+        Bx = patch_rows.shape[1]
+        x_in = F.linear(patch_rows.reshape(n * Bx, -1), p["x_embedder.proj.1.weight"]).view(n, Bx, D)
+        mods, shift_f, scale_f = self.time_modulation(t_B_T)
+        cos, sin = self.rope_tables(geo)
+        cp = self.cp_group
+        cp_size = 1 if cp is None else torch.distributed.get_world_size(cp)
+
+        def mod(i, j):  # (shift, scale, gate) bf16 [B, T, D] views of block i, sub-layer j
+            m = mods[i, j]
+            return m[..., :D], m[..., D:2 * D], m[..., 2 * D:]
+
+        common = dict(n_tok=n, B=B, tok0=geo.tok0, hw=geo.hw)
+        sh, sc, _ = mod(0, 0)
+        x = x_in
+        h = N.ln_mod(x, sh, sc, x_st=Bx * D, x_sb=0 if Bx == 1 else D, **common)
+        y = None
+        gate_prev = None
+        scale_attn = hd ** -0.5
+        for i in range(cfg.num_blocks):
+            pre = f"blocks.{i}."
+            # ---- self attention
+            qkv = F.linear(h.view(n * B, D), self.w_qkv[i])  # [n*B, 3D]
+            N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=0, weight=p[pre + "self_attn.q_norm.weight"],
+                                cos=cos, sin=sin)
+            q = qkv.view(n, B, 3 * D)[:, :, :D].view(n, B, H, hd).transpose(0, 1)
+            if cp is None or cp_size == 1:
+                N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=D,
+                                    weight=p[pre + "self_attn.k_norm.weight"], cos=cos, sin=sin)
+                kk = qkv.view(n, B, 3 * D)[:, :, D:2 * D].view(n, B, H, hd).transpose(0, 1)
+                vv = qkv.view(n, B, 3 * D)[:, :, 2 * D:].view(n, B, H, hd).transpose(0, 1)
+            else:
+                kv_loc = torch.empty((n, B, 2 * D), dtype=BF16, device=self.device)
+                N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=D,
+                                    weight=p[pre + "self_attn.k_norm.weight"], cos=cos, sin=sin,
+                                    out2=kv_loc, out2_stride=2 * D)
+                N.copy_rows(qkv, 3 * D, kv_loc.view(n * B, 2 * D)[:, D:], 2 * D, n * B, D, src_offset=2 * D)
+                kv = torch.empty((cp_size * n, B, 2 * D), dtype=BF16, device=self.device)
+                torch.distributed.all_gather_into_tensor(kv, kv_loc, group=cp)
+                kk = kv[:, :, :D].view(cp_size * n, B, H, hd).transpose(0, 1)
+                vv = kv[:, :, D:].view(cp_size * n, B, H, hd).transpose(0, 1)
+            o = torch.empty((n, B, D), dtype=BF16, device=self.device)
+            N.attn_fwd(q, kk, vv, out=o.view(n, B, H, hd).transpose(0, 1), softmax_scale=scale_attn)
+            y = F.linear(o.view(n * B, D), p[pre + "self_attn.output_proj.weight"])
+            # ---- x += g_sa * y ; LN-mod for cross attention
+            _, _, g_sa = mod(i, 0)
+            sh, sc, _ = mod(i, 1)
+            x_new = torch.empty((n, B, D), dtype=BF16, device=self.device)
+            h = N.ln_mod(x, sh, sc, x_st=(Bx if i == 0 else B) * D, x_sb=(0 if (i == 0 and Bx == 1) else D),
+                         y=y, gate=g_sa, x_out=x_new, **common)
+            x = x_new
+            # ---- cross attention
+            qc = F.linear(h.view(n * B, D), p[pre + "cross_attn.q_proj.weight"])
+            N.head_rmsnorm_rope(qc, n_rows=n * B, B=B, H=H, head_off=0, weight=p[pre + "cross_attn.q_norm.weight"])
+            o = torch.empty((n, B, D), dtype=BF16, device=self.device)
+            N.attn_fwd(qc.view(n, B, H, hd).transpose(0, 1), ctx.k[i], ctx.v[i],
+                       out=o.view(n, B, H, hd).transpose(0, 1), softmax_scale=scale_attn)
+            y = F.linear(o.view(n * B, D), p[pre + "cross_attn.output_proj.weight"])
+            _, _, g_ca = mod(i, 1)
+            sh, sc, _ = mod(i, 2)
+            x_new = torch.empty((n, B, D), dtype=BF16, device=self.device)
+            h = N.ln_mod(x, sh, sc, x_st=B * D, x_sb=D, y=y, gate=g_ca, x_out=x_new, **common)
+            x = x_new
+            # ---- MLP
+            u = F.linear(h.view(n * B, D), p[pre + "mlp.layer1.weight"])
+            N.gelu_(u)
+            y = F.linear(u, p[pre + "mlp.layer2.weight"])
+            del u
+            _, _, gate_prev = mod(i, 2)
+            if i + 1 < cfg.num_blocks:
+                sh, sc, _ = mod(i + 1, 0)
+                x_new = torch.empty((n, B, D), dtype=BF16, device=self.device)
+                h = N.ln_mod(x, sh, sc, x_st=B * D, x_sb=D, y=y, gate=gate_prev, x_out=x_new, **common)
+                x = x_new
+        # ---- final layer (fp32 autocast): x + g*y -> LN -> modulate -> Linear(D -> 64)
+        xf = N.final_ln_mod(x, shift_f, scale_f, y=y, gate=gate_prev, **common)
+        out = F.linear(xf.view(n * B, D), self.w_final)
+        return out.view(n, B, -1)
+
+    # ---------------------------------------------------------------- reference-compatible forward
+    @torch.no_grad()
+    def forward(self, x_B_C_T_H_W: torch.Tensor, timesteps_B_T: torch.Tensor, crossattn_emb: torch.Tensor,
+                condition_video_input_mask_B_C_T_H_W: Optional[torch.Tensor] = None, fps=None,
+                padding_mask: Optional[torch.Tensor] = None, data_type=None, **kwargs) -> torch.Tensor:
+        """MinimalV1LVGDiT.forward signature (minimal_v1_lvg_dit.py:31-62) -> [B, C, T, H, W] fp32."""
+        cfg = self.cfg
+        B, C, T, Hl, Wl = x_B_C_T_H_W.shape
+        Hp, Wp = Hl // cfg.patch_spatial, Wl // cfg.patch_spatial
+        geo = Geometry(T=T, Hp=Hp, Wp=Wp, tok0=0, n_tok=T * Hp * Wp)
+        x = x_B_C_T_H_W.to(self.device, BF16)
+        if condition_video_input_mask_B_C_T_H_W is None:
+            mask = torch.zeros(B, 1, T, Hl, Wl, dtype=BF16, device=self.device)
+        else:
+            mask = condition_video_input_mask_B_C_T_H_W.to(self.device).to(BF16)
+        chans = [x, mask]
+        if cfg.concat_padding_mask:
+            pm = padding_mask if padding_mask is not None else torch.zeros(B, 1, Hl, Wl)
+            pm = F.interpolate(pm.to(self.device).float(), size=(Hl, Wl), mode="nearest").to(BF16)
+            chans.append(pm[:, :, None].expand(B, 1, T, Hl, Wl))
+        xc = torch.cat(chans, dim=1)
+        # b c t (h m) (w n) -> (t h w) b (c m n)
+        rows = xc.view(B, xc.shape[1], T, Hp, 2, Wp, 2).permute(2, 3, 5, 0, 1, 4, 6).reshape(geo.L, B, -1)
+        ctx = self.prepare_context(crossattn_emb)
+        if timesteps_B_T.ndim == 1:
+            timesteps_B_T = timesteps_B_T.unsqueeze(1)
+        t = timesteps_B_T.to(self.device).float() * cfg.timestep_scale
+        if t.shape[1] == 1 and T > 1:
+            t = t.expand(B, T).contiguous()
+        out = self.forward_tokens(rows.contiguous(), t, ctx, geo)  # [L, B, 64] (p1 p2 C)
+        out = out.view(T, Hp, Wp, B, 2, 2, C).permute(3, 6, 0, 1, 4, 2, 5)
+        return out.reshape(B, C, T, Hl, Wl).float()
+
+    __call__ = forward

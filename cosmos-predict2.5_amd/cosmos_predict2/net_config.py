@@ -1,0 +1,100 @@
+"""Network / sampler hyper-parameters of the Cosmos-Predict2.5 checkpoints this build serves.
+
+Values follow the reference's registered configs:
+  * net: COSMOS_V1_2B_NET_MININET / COSMOS_V1_14B_NET_MININET
+    (cosmos_predict2/_src/predict2/configs/video2world/defaults/net.py:58-94) with the rectified-flow
+    experiment overrides (configs/video2world/experiment/reason_embeddings/
+    model_2B_reason_1p1_rectified_flow.py:300-338, model_14b_reason_1p1_rectified_flow.py:322-344);
+  * sampler: Stage-c_pt_4-Index-2-Size-2B-Res-720-Fps-16-Note-rf_with_edm_ckpt
+    (configs/video2world/experiment/specialized_model/SFT_2B_RF.py:752-768: Karras sigmas,
+    conditional_frame_timestep 0.1) for 2B post-trained; shift-5 linspace for the pre-trained models.
+"""
+from __future__ import annotations
+
+import dataclasses
+from dataclasses import dataclass, field
+
+
+@dataclass(frozen=True)
+class DiTConfig:
+    model_channels: int = 2048
+    num_heads: int = 16
+    num_blocks: int = 28
+    mlp_ratio: float = 4.0
+    in_channels: int = 16  # latent channels (MinimalV1LVGDiT adds +1 for the condition mask)
+    out_channels: int = 16
+    patch_spatial: int = 2
+    patch_temporal: int = 1
+    concat_padding_mask: bool = True
+    crossattn_emb_channels: int = 1024
+    use_crossattn_projection: bool = True
+    crossattn_proj_in_channels: int = 100352
+    adaln_lora_dim: int = 256
+    max_img_h: int = 240
+    max_img_w: int = 240
+    max_frames: int = 128
+    rope_h_extrapolation_ratio: float = 3.0
+    rope_w_extrapolation_ratio: float = 3.0
+    rope_t_extrapolation_ratio: float = 1.0
+    rope_enable_fps_modulation: bool = False
+    timestep_scale: float = 0.001
+    use_wan_fp32_strategy: bool = True
+
+    @property
+    def head_dim(self) -> int:
+        return self.model_channels // self.num_heads
+
+    @property
+    def patch_features(self) -> int:
+        # (in_channels + cond mask + padding mask) * p_t * p_s * p_s
+        return (self.in_channels + 1 + int(self.concat_padding_mask)) * self.patch_temporal * self.patch_spatial ** 2
+
+    @property
+    def mlp_hidden(self) -> int:
+        return int(self.model_channels * self.mlp_ratio)
+
+    def replace(self, **kw) -> "DiTConfig":
+        return dataclasses.replace(self, **kw)
+
+
+@dataclass(frozen=True)
+class SamplerConfig:
+    """Text2WorldModelRectifiedFlowConfig / Video2WorldModelRectifiedFlowConfig fields used at inference."""
+
+    state_ch: int = 16
+    state_t: int = 24
+    shift: float = 5.0
+    use_kerras_sigma_at_inference: bool = False
+    conditional_frame_timestep: float = -1.0
+    denoise_replace_gt_frames: bool = True
+    cfg_mode: str = "video2world"  # "video2world": c + g(c-u) ; "text2world": u + g(c-u)
+    resolution: str = "720"
+
+
+DIT_2B = DiTConfig()
+DIT_14B = DiTConfig(model_channels=5120, num_heads=40, num_blocks=36)
+
+SAMPLER_2B_POST_TRAINED = SamplerConfig(use_kerras_sigma_at_inference=True, conditional_frame_timestep=0.1)
+SAMPLER_PRE_TRAINED = SamplerConfig()
+
+# model name (cosmos_predict2/config.py ModelKey.name) -> (net, sampler)
+MODELS = {
+    "2B/post-trained": (DIT_2B, SAMPLER_2B_POST_TRAINED),
+    "2B/pre-trained": (DIT_2B, SAMPLER_PRE_TRAINED),
+    "14B/pre-trained": (DIT_14B, SAMPLER_PRE_TRAINED),
+}
+
+# Subset of VIDEO_RES_SIZE_INFO (cosmos_predict2/_src/predict2/datasets/utils.py:44-67); the model's
+# default resolution is the "9,16" entry read as (H, W) (text2world_model_rectified_flow.py:872-873).
+VIDEO_RES_SIZE_INFO = {
+    "720": {"1,1": (960, 960), "4,3": (960, 704), "3,4": (704, 960), "16,9": (1280, 704), "9,16": (704, 1280)},
+    "480": {"1,1": (480, 480), "4,3": (640, 480), "3,4": (480, 640), "16,9": (768, 432), "9,16": (432, 768)},
+    "256": {"1,1": (256, 256), "4,3": (320, 256), "3,4": (256, 320), "16,9": (320, 192), "9,16": (192, 320)},
+}
+
+
+def tiny_dit(**kw) -> DiTConfig:
+    """A small configuration with the 2B layout for tests (head dim 128)."""
+    base = DiTConfig(model_channels=512, num_heads=4, num_blocks=2, crossattn_emb_channels=256,
+                     crossattn_proj_in_channels=384, adaln_lora_dim=64)
+    return base.replace(**kw)

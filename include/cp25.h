@@ -1,0 +1,116 @@
+/*
+ * cp25.h -- C ABI of the MI355X-native cosmos-predict2.5 sampler kernels (libcp25.so, gfx950).
+ *
+ * This is the drop-in boundary below the reference's Python operator plug points. Each entry point
+ * names the reference interface it replaces (paths relative to the reference repository root,
+ * cosmos_predict2/_src/predict2/...). The Python side (cosmos-predict2.5_amd/cosmos_predict2/_native.py)
+ * binds these with ctypes; INTEGRATION.md shows the binding a reference maintainer would add.
+ *
+ * Contract for every function:
+ *   - pointers are device pointers (HBM); strides and sizes are in ELEMENTS, int64;
+ *   - bf16 tensors are passed as void* holding IEEE bfloat16 bits, fp32 tensors as float*;
+ *   - the call is stream-ordered on `stream`, never allocates, never synchronises, is re-entrant
+ *     and hipGraph-capturable; the caller owns all memory (PyTorch's caching allocator);
+ *   - returns 0 (CP25_OK) or a negative code checked on the host before launching:
+ *       -22 bad shape/stride/pointer, -95 unsupported dtype/head-dim/width, -5 launch failure.
+ */
+#ifndef CP25_H
+#define CP25_H
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- attention
+ * softmax(Q K^T * softmax_scale) V, non-causal, no mask; bf16 in/out, fp32 accumulation.
+ * q: [B, Lq, H, D] addressed by q_strides = {batch, token, head} (head dim contiguous), same for
+ * k/v ([B, Lk, H, D]) and o ([B, Lq, H, D]). D must be 128. All strides multiples of 8 elements.
+ * Replaces: networks/attention.py:90-181 `attention()` as called by MinimalA2AAttnOp
+ * (networks/a2a_cp.py:208-219) for self-attention (minimal_v4_dit.py:431) and cross-attention
+ * (minimal_v4_dit.py:1216-1226; Lk = 512 text tokens). */
+int cp25_attn_fwd(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq, int Lk, int D,
+                  const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
+                  const int64_t* o_strides, float softmax_scale, hipStream_t stream);
+
+/* ---------------------------------------------------------------- DiT block elementwise
+ * Activations are token-major [n_tok, B, D] bf16 (batch inner). Row (tok, b) uses modulation row
+ * (b, t) with t = (tok0 + tok) / hw (frame index; tok0 = first global token of this CP shard).
+ *
+ * cp25_ln_mod: if y != NULL first x' = x + gate * y (two bf16 roundings, stored to x_out [n_tok,B,D]);
+ * then h_out = LayerNorm(x', no affine, eps) * (1 + scale) + shift with the reference's bf16
+ * rounding after every torch op. x is read as x[tok * x_st + b * x_sb] (x_sb = 0 broadcasts one
+ * row to every batch entry). gate/shift/scale: bf16, element (b, t, d) at b*mod_sb + t*mod_st + d.
+ * D in {512, 1024, 2048, 4096, 5120}.
+ * Replaces: Block.forward _fn + gated residuals, minimal_v4_dit.py:1171-1179, 1204, 1237, 1246. */
+int cp25_ln_mod(const void* x, int64_t x_st, int64_t x_sb, const void* y, const void* gate, const void* shift,
+                const void* scale, int64_t mod_sb, int64_t mod_st, void* x_out, void* h_out, int64_t n_tok, int B,
+                int D, int64_t tok0, int64_t hw, float eps, hipStream_t stream);
+
+/* Final layer prologue under the reference's fp32 autocast: [x' = x + gate*y (bf16)], then
+ * out = LayerNorm_fp32(x') * (1 + scale) + shift in fp32 (shift/scale fp32).
+ * Replaces: FinalLayer.forward, minimal_v4_dit.py:974-991 (and the last block's MLP residual :1246). */
+int cp25_final_ln_mod(const void* x, const void* y, const void* gate, int64_t gmod_sb, int64_t gmod_st,
+                      const float* shift, const float* scale, int64_t mod_sb, int64_t mod_st, float* out,
+                      int64_t n_tok, int B, int D, int64_t tok0, int64_t hw, float eps, hipStream_t stream);
+
+/* In-place per-head RMSNorm (weight[128] bf16, eps) of heads [head_off, head_off + H*128) of every
+ * row of a bf16 [n_rows, row_stride] buffer, then (if cos_tab != NULL) rotate-half RoPE in fp32
+ * with cos/sin tables [n_tok, 64] fp32 indexed by token = row / B, result rounded to bf16.
+ * If out2 != NULL the result is also written to out2[row * out2_stride + h*128 + d].
+ * Replaces: Attention.compute_qkv norm + TE RoPE + attention() recast, minimal_v4_dit.py:410-420,
+ * networks/attention.py:107-109. */
+int cp25_head_rmsnorm_rope(void* buf, int64_t row_stride, int64_t n_rows, int B, int H, int head_off,
+                           const void* weight, const float* cos_tab, const float* sin_tab, void* out2,
+                           int64_t out2_stride, float eps, hipStream_t stream);
+
+/* dst[r, 0:width] = src[r, 0:width] for bf16 rows (K/V export before the CP all-gather). */
+int cp25_copy_rows(const void* src, int64_t src_stride, void* dst, int64_t dst_stride, int64_t n_rows, int64_t width,
+                   hipStream_t stream);
+
+/* In-place exact (erf) GELU on n bf16 values (n % 8 == 0).
+ * Replaces: GPT2FeedForward activation, minimal_v4_dit.py:249-254. */
+int cp25_gelu(void* x, int64_t n, hipStream_t stream);
+
+/* Latents live in "patch layout" [n_tok, 64] fp32, element (tok, p*16 + c), p = p1*2 + p2 (the
+ * final layer's "(p1 p2 t C)" order). cp25_patchify builds the x_embedder input rows [n_tok, 72]
+ * bf16 (feature c*4 + p): channels 0..15 = gt*mask + x*(1-mask) (gt may be NULL), channel 16 = the
+ * per-frame condition mask, channel 17 = padding mask (pad_mask [n_tok, 4] bf16 or NULL = 0).
+ * Replaces: video2world_model_rectified_flow.py:105-107, minimal_v1_lvg_dit.py:46,
+ * minimal_v4_dit.py:1547-1554 and PatchEmbed's rearrange (:873-878). */
+int cp25_patchify(const float* xs, const float* gt, const float* frame_mask, const void* pad_mask, void* out,
+                  int64_t n_tok, int64_t tok0, int64_t hw, hipStream_t stream);
+
+/* v_out[tok, j] from the final-layer output net [n_tok, B, 64] fp32 (B = 1 or 2 = cond, uncond):
+ * per branch v_b = (noise - gt) * mask + net_b * (1 - mask) (skipped if gt == NULL), then
+ * cfg_mode 0: v = v_c + guidance (v_c - v_u)   (Video2World, video2world_model_rectified_flow.py:209)
+ * cfg_mode 1: v = v_u + guidance (v_c - v_u)   (Text2World, text2world_model_rectified_flow.py:511)
+ * Replaces: Video2WorldModelRectifiedFlow.denoise :131-136, velocity_fn :206-210, MiniTrainDIT.unpatchify. */
+int cp25_cfg_velocity(const float* net, int B, const float* noise, const float* gt, const float* frame_mask,
+                      float guidance, int cfg_mode, float* v_out, int64_t n_tok, int64_t tok0, int64_t hw,
+                      hipStream_t stream);
+
+/* ---------------------------------------------------------------- UniPC sampler update
+ * Host-computed fp32 coefficients of one FlowUniPCMultistepScheduler.step. */
+typedef struct cp25_unipc_params {
+  float sigma;      /* sigmas[step_index] */
+  int use_corr;     /* corrector active */
+  int order_c;      /* 1 or 2 */
+  float c_a, c_b, c_c, c_inv_rk, c_rho0, c_rho_last;
+  int order_p;      /* 1 or 2 */
+  float p_a, p_b, p_c, p_inv_rk, p_rho0;
+} cp25_unipc_params;
+
+/* One fused, bit-exact UniPC step over n fp32 elements, in place on x (sample), m0/m1 (the two
+ * converted model outputs of the history) and last (last_sample); v = the velocity prediction.
+ * Replaces: FlowUniPCMultistepScheduler.step elementwise math, models/fm_solvers_unipc.py:266-335,
+ * 337-464, 466-601, 630-713. */
+int cp25_unipc_step(float* x, const float* v, float* m0, float* m1, float* last, int64_t n,
+                    const cp25_unipc_params* params, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CP25_H */

@@ -1,0 +1,210 @@
+"""DiT denoiser forward restatement (CPU) — TEST INFRASTRUCTURE (see oracle/__init__.py).
+
+Restates MinimalV1LVGDiT.forward -> MiniTrainDIT.forward as the reference runs it at inference:
+net weights and float buffers in bf16 (utils/model_loader.py:88-90 + on_train_start), bf16 torch ops
+for the block body, fp32 autocast for the t-embedding, AdaLN modulation and final layer
+(use_wan_fp32_strategy, minimal_v4_dit.py:974-995, 1136-1154, 1615-1619), q/k upcast to fp32 for
+RoPE (:415-419) and recast to bf16 by attention() (networks/attention.py:107-109).
+
+Paths relative to cosmos_predict2/_src/predict2/networks/ unless stated:
+  minimal_v1_lvg_dit.py:31-62      condition-mask channel, timestep scale
+  minimal_v4_dit.py:1517-1565      padding mask + PatchEmbed (:846-913)
+  minimal_v4_dit.py:539-667        3D RoPE (bf16 range buffers, F8)
+  minimal_v4_dit.py:727-788        Timesteps / TimestepEmbedding (adaln-lora)
+  minimal_v4_dit.py:1124-1247      Block.forward
+  minimal_v4_dit.py:916-995        FinalLayer
+  minimal_v4_dit.py:1567-1575      unpatchify
+Third-party numerics restated by their standard formulas (parity unpinned):
+TE RMSNorm (fp32 math, one rounding of (x*rstd)*w), TE fused RoPE (rotate-half, fp32), SDPA
+(fp32 softmax, bf16 output).
+
+Config: a dict with the DiTConfig field names (cosmos_predict2/net_config.py).
+Weights: a state dict with the reference's `net.` key layout, bf16 tensors.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+def _w(sd, name):
+    return sd["net." + name]
+
+
+def te_rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-6) -> torch.Tensor:
+    xf = x.float()
+    rstd = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    return ((xf * rstd) * w.float()).to(x.dtype)
+
+
+def rope_freqs(cfg: dict, T: int, H: int, W: int) -> torch.Tensor:
+    """VideoRopePosition3DEmb.generate_embeddings with bf16 buffers -> [T*H*W, 128] fp32."""
+    dim = cfg["model_channels"] // cfg["num_heads"]
+    dim_h = dim // 6 * 2
+    dim_t = dim - 2 * dim_h
+    # buffers (registered fp32, cast to bf16 with the net)
+    spatial_range = (torch.arange(0, dim_h, 2)[: dim_h // 2].float() / dim_h).to(BF16)
+    temporal_range = (torch.arange(0, dim_t, 2)[: dim_t // 2].float() / dim_t).to(BF16)
+    len_h = cfg["max_img_h"] // cfg["patch_spatial"]
+    len_w = cfg["max_img_w"] // cfg["patch_spatial"]
+    len_t = cfg["max_frames"] // cfg["patch_temporal"]
+    seq = torch.arange(max(len_h, len_w, len_t)).float().to(BF16)
+    h_theta = 10000.0 * cfg["rope_h_extrapolation_ratio"] ** (dim_h / (dim_h - 2))
+    w_theta = 10000.0 * cfg["rope_w_extrapolation_ratio"] ** (dim_h / (dim_h - 2))
+    t_theta = 10000.0 * cfg["rope_t_extrapolation_ratio"] ** (dim_t / (dim_t - 2))
+    fh = 1.0 / (h_theta ** spatial_range.float())
+    fw = 1.0 / (w_theta ** spatial_range.float())
+    ft = 1.0 / (t_theta ** temporal_range.float())
+    eh = torch.outer(seq[:H], fh)
+    ew = torch.outer(seq[:W], fw)
+    et = torch.outer(seq[:T], ft)
+    grid = torch.cat(
+        [
+            et[:, None, None, :].expand(T, H, W, -1),
+            eh[None, :, None, :].expand(T, H, W, -1),
+            ew[None, None, :, :].expand(T, H, W, -1),
+        ]
+        * 2,
+        dim=-1,
+    )
+    return grid.reshape(T * H * W, dim).float()
+
+
+def apply_rope(x: torch.Tensor, freqs: torch.Tensor) -> torch.Tensor:
+    """rotate-half RoPE in fp32: x [B, L, H, D] fp32, freqs [L, D]."""
+    d2 = x.shape[-1] // 2
+    rot = torch.cat([-x[..., d2:], x[..., :d2]], dim=-1)
+    c = torch.cos(freqs)[None, :, None, :]
+    s = torch.sin(freqs)[None, :, None, :]
+    return x * c + rot * s
+
+
+def sdpa(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, chunk: int = 4096) -> torch.Tensor:
+    """[B, S, H, D] bf16 -> [B, S, H*D] bf16 with fp32 softmax (query-chunked for memory)."""
+    B, Lq, H, D = q.shape
+    kf = k.float().transpose(1, 2)
+    vf = v.float().transpose(1, 2)
+    outs = []
+    for s0 in range(0, Lq, chunk):
+        qf = q[:, s0 : s0 + chunk].float().transpose(1, 2)
+        p = torch.softmax(torch.matmul(qf, kf.transpose(-1, -2)) * (D ** -0.5), dim=-1)
+        outs.append(torch.matmul(p, vf).transpose(1, 2))
+    o = torch.cat(outs, dim=1)
+    return o.reshape(B, Lq, H * D).to(BF16)
+
+
+def _lin(x, w, b=None):
+    return F.linear(x, w, b)
+
+
+def timestep_embedding(cfg, sd, t_B_T: torch.Tensor):
+    """Timesteps + TimestepEmbedding(adaln-lora) + t_embedding_norm, fp32 (autocast)."""
+    D = cfg["model_channels"]
+    half = D // 2
+    expo = -math.log(10000) * torch.arange(half, dtype=F32) / (half - 0.0)
+    emb = t_B_T.flatten().float()[:, None] * torch.exp(expo)[None, :]
+    sincos = torch.cat([torch.cos(emb), torch.sin(emb)], dim=-1).reshape(t_B_T.shape[0], t_B_T.shape[1], D)
+    h = F.silu(_lin(sincos, _w(sd, "t_embedder.1.linear_1.weight").float()))
+    lora = _lin(h, _w(sd, "t_embedder.1.linear_2.weight").float())
+    emb_norm = te_rmsnorm(sincos, _w(sd, "t_embedding_norm.weight"))
+    return emb_norm, lora
+
+
+def adaln(sd, prefix, emb, lora, n_chunks=3):
+    h = F.silu(emb)
+    h = _lin(h, _w(sd, prefix + ".1.weight").float())
+    h = _lin(h, _w(sd, prefix + ".2.weight").float())
+    return (h + lora[..., : h.shape[-1]]).chunk(n_chunks, dim=-1)
+
+
+def ln_mod(x, shift, scale):
+    # nn.LayerNorm(no affine, eps 1e-6) on bf16 -> bf16, then bf16 ops (minimal_v4_dit.py:1171-1172)
+    return F.layer_norm(x, (x.shape[-1],), eps=1e-6) * (1 + scale) + shift
+
+
+def block_forward(cfg, sd, i, x, emb, lora, ctx, freqs):
+    """Block.forward, x [B, T, H, W, D] bf16."""
+    p = f"blocks.{i}."
+    nh, hd = cfg["num_heads"], cfg["model_channels"] // cfg["num_heads"]
+    sh_sa, sc_sa, g_sa = adaln(sd, p + "adaln_modulation_self_attn", emb, lora)
+    sh_ca, sc_ca, g_ca = adaln(sd, p + "adaln_modulation_cross_attn", emb, lora)
+    sh_ml, sc_ml, g_ml = adaln(sd, p + "adaln_modulation_mlp", emb, lora)
+    cvt = lambda t: t[:, :, None, None, :].to(BF16)  # noqa: E731
+    sh_sa, sc_sa, g_sa, sh_ca, sc_ca, g_ca, sh_ml, sc_ml, g_ml = map(
+        cvt, (sh_sa, sc_sa, g_sa, sh_ca, sc_ca, g_ca, sh_ml, sc_ml, g_ml)
+    )
+    B, T, H, W, D = x.shape
+
+    # self attention
+    h = ln_mod(x, sh_sa, sc_sa).reshape(B, T * H * W, D)
+    q = _lin(h, _w(sd, p + "self_attn.q_proj.weight")).reshape(B, -1, nh, hd)
+    k = _lin(h, _w(sd, p + "self_attn.k_proj.weight")).reshape(B, -1, nh, hd)
+    v = _lin(h, _w(sd, p + "self_attn.v_proj.weight")).reshape(B, -1, nh, hd)
+    q = te_rmsnorm(q, _w(sd, p + "self_attn.q_norm.weight")).float()
+    k = te_rmsnorm(k, _w(sd, p + "self_attn.k_norm.weight")).float()
+    q = apply_rope(q, freqs)
+    k = apply_rope(k, freqs)
+    o = sdpa(q.to(BF16), k.to(BF16), v.to(BF16))
+    o = _lin(o, _w(sd, p + "self_attn.output_proj.weight")).reshape(B, T, H, W, D)
+    x = x + g_sa * o
+
+    # cross attention (no RoPE)
+    h = ln_mod(x, sh_ca, sc_ca).reshape(B, T * H * W, D)
+    q = _lin(h, _w(sd, p + "cross_attn.q_proj.weight")).reshape(B, -1, nh, hd)
+    k = _lin(ctx, _w(sd, p + "cross_attn.k_proj.weight")).reshape(B, -1, nh, hd)
+    v = _lin(ctx, _w(sd, p + "cross_attn.v_proj.weight")).reshape(B, -1, nh, hd)
+    q = te_rmsnorm(q, _w(sd, p + "cross_attn.q_norm.weight"))
+    k = te_rmsnorm(k, _w(sd, p + "cross_attn.k_norm.weight"))
+    o = sdpa(q, k, v)
+    o = _lin(o, _w(sd, p + "cross_attn.output_proj.weight")).reshape(B, T, H, W, D)
+    x = o * g_ca + x
+
+    # MLP
+    h = ln_mod(x, sh_ml, sc_ml)
+    u = F.gelu(_lin(h, _w(sd, p + "mlp.layer1.weight")))
+    y = _lin(u, _w(sd, p + "mlp.layer2.weight"))
+    return x + g_ml * y
+
+
+def dit_forward(cfg: dict, sd: dict, x_B_C_T_H_W: torch.Tensor, timesteps_B_T: torch.Tensor,
+                crossattn_emb: torch.Tensor, cond_mask_B_1_T_H_W: torch.Tensor,
+                padding_mask_B_1_H_W: torch.Tensor | None = None) -> torch.Tensor:
+    """-> velocity [B, C, T, H, W] fp32 (the model applies .float(), text2world_model_rectified_flow.py:860)."""
+    x = x_B_C_T_H_W.to(BF16)
+    B, C, T, Hl, Wl = x.shape
+    x = torch.cat([x, cond_mask_B_1_T_H_W.to(BF16)], dim=1)  # minimal_v1_lvg_dit.py:46
+    t = timesteps_B_T * cfg["timestep_scale"]
+    if cfg["concat_padding_mask"]:
+        pm = padding_mask_B_1_H_W if padding_mask_B_1_H_W is not None else torch.zeros(B, 1, Hl, Wl)
+        pm = F.interpolate(pm.float(), size=(Hl, Wl), mode="nearest").to(BF16)
+        x = torch.cat([x, pm[:, :, None].expand(B, 1, T, Hl, Wl)], dim=1)
+    ps, pt = cfg["patch_spatial"], cfg["patch_temporal"]
+    Tp, Hp, Wp = T // pt, Hl // ps, Wl // ps
+    # b c (t r) (h m) (w n) -> b t h w (c r m n)
+    xp = x.reshape(B, x.shape[1], Tp, pt, Hp, ps, Wp, ps).permute(0, 2, 4, 6, 1, 3, 5, 7)
+    xp = xp.reshape(B, Tp, Hp, Wp, -1)
+    x = _lin(xp, _w(sd, "x_embedder.proj.1.weight"))
+    freqs = rope_freqs(cfg, Tp, Hp, Wp)
+
+    ctx = crossattn_emb.to(BF16)
+    if cfg["use_crossattn_projection"]:
+        ctx = F.gelu(_lin(ctx, _w(sd, "crossattn_proj.0.weight"), _w(sd, "crossattn_proj.0.bias")))
+
+    emb, lora = timestep_embedding(cfg, sd, t)
+    for i in range(cfg["num_blocks"]):
+        x = block_forward(cfg, sd, i, x, emb, lora, ctx, freqs)
+
+    # final layer (fp32 autocast)
+    D = cfg["model_channels"]
+    sh, sc = adaln(sd, "final_layer.adaln_modulation", emb, lora[..., : 2 * D], n_chunks=2)
+    xf = F.layer_norm(x.float(), (D,), eps=1e-6)
+    xf = xf * (1 + sc[:, :, None, None, :]) + sh[:, :, None, None, :]
+    out = _lin(xf, _w(sd, "final_layer.linear.weight").float())  # [B,Tp,Hp,Wp, p1*p2*pt*C]
+    Cout = cfg["out_channels"]
+    out = out.reshape(B, Tp, Hp, Wp, ps, ps, pt, Cout).permute(0, 7, 1, 6, 2, 4, 3, 5)
+    return out.reshape(B, Cout, Tp * pt, Hp * ps, Wp * ps).float()

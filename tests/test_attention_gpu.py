@@ -1,0 +1,96 @@
+"""Parity of the HIP flash-attention kernel (cp25_attn_fwd) against an fp32 reference of the same op.
+
+Reference op: networks/attention.py:90-181 — q/k/v recast to bf16, softmax(q k^T / sqrt(D)) v.
+Oracle here: the same formula in fp32 on the bf16 inputs, output rounded to bf16.
+Tolerance: rel-L2 <= 4e-3 and max-abs <= 3e-2. Derivation: every flash-attention kernel the
+reference dispatches to (FA2/FA3/cuDNN) rounds the softmax numerator P to bf16 before P.V, which alone
+is a ~2^-9/sqrt(3) ~ 1.1e-3 relative error on O, plus bf16 rounding flips of the output itself;
+measured 2.2e-3 at Lk = 64 on random data.
+"""
+import math
+
+import pytest
+import torch
+
+from cosmos_predict2 import _native as N
+
+pytestmark = pytest.mark.gpu
+
+TOL = 4e-3
+
+
+def ref_attention(q, k, v, scale=None):
+    # q [B,Lq,H,D] -> fp32 math
+    qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k, v))
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * (scale if scale is not None else q.shape[-1] ** -0.5)
+    p = torch.softmax(s, dim=-1)
+    o = torch.matmul(p, vf).transpose(1, 2)
+    return o.to(torch.bfloat16)
+
+
+def rel_l2(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize(
+    "B,H,Lq,Lk",
+    [(1, 1, 32, 64), (2, 3, 300, 77), (1, 2, 256, 512), (2, 2, 1000, 1030), (1, 16, 257, 768), (1, 1, 5, 3)],
+)
+def test_attn_matches_fp32(device, B, H, Lq, Lk):
+    g = torch.Generator(device="cpu").manual_seed(1234 + Lq + Lk)
+    q = torch.randn(B, Lq, H, 128, generator=g).to(device, torch.bfloat16)
+    k = torch.randn(B, Lk, H, 128, generator=g).to(device, torch.bfloat16)
+    v = torch.randn(B, Lk, H, 128, generator=g).to(device, torch.bfloat16)
+    o = N.attn_fwd(q, k, v)
+    torch.cuda.synchronize()
+    ref = ref_attention(q, k, v)
+    assert torch.isfinite(o.float()).all()
+    assert rel_l2(o, ref) <= TOL, rel_l2(o, ref)
+    assert (o.float() - ref.float()).abs().max().item() <= 3e-2
+
+
+def test_attn_strided_qkv_buffer(device):
+    """q/k/v as views of one fused [L, B, 3, H, 128] projection buffer (the DiT's token-major layout)."""
+    L, B, H = 700, 2, 4
+    g = torch.Generator(device="cpu").manual_seed(7)
+    qkv = torch.randn(L, B, 3, H, 128, generator=g).to(device, torch.bfloat16)
+    q = qkv[:, :, 0].transpose(0, 1)  # [B, L, H, D] view
+    k = qkv[:, :, 1].transpose(0, 1)
+    v = qkv[:, :, 2].transpose(0, 1)
+    out = torch.empty(L, B, H, 128, dtype=torch.bfloat16, device=device)
+    N.attn_fwd(q, k, v, out=out.transpose(0, 1))
+    ref = ref_attention(q.contiguous(), k.contiguous(), v.contiguous())
+    assert rel_l2(out.transpose(0, 1), ref) <= TOL
+
+
+def test_attn_rescale_branch(device):
+    """Force the online-softmax running max to jump late (rule 26): a spiked key in the last tile."""
+    B, H, Lq, Lk = 1, 2, 256, 640
+    g = torch.Generator(device="cpu").manual_seed(3)
+    q = torch.randn(B, Lq, H, 128, generator=g)
+    k = torch.randn(B, Lk, H, 128, generator=g) * 0.1
+    v = torch.randn(B, Lk, H, 128, generator=g)
+    k[:, Lk - 5] = q[:, 17] * 3.0  # one key aligned with query 17 in the last tile
+    k[:, 100] = -q[:, 40] * 2.0
+    q, k, v = (t.to(device, torch.bfloat16) for t in (q, k, v))
+    o = N.attn_fwd(q, k, v)
+    ref = ref_attention(q, k, v)
+    assert rel_l2(o, ref) <= TOL
+
+
+def test_attn_cross_shape(device):
+    """Cross-attention: video tokens against 512 text tokens."""
+    B, H, Lq, Lk = 2, 16, 2048, 512
+    g = torch.Generator(device="cpu").manual_seed(11)
+    q = torch.randn(B, Lq, H, 128, generator=g).to(device, torch.bfloat16)
+    k = torch.randn(B, Lk, H, 128, generator=g).to(device, torch.bfloat16)
+    v = torch.randn(B, Lk, H, 128, generator=g).to(device, torch.bfloat16)
+    assert rel_l2(N.attn_fwd(q, k, v), ref_attention(q, k, v)) <= TOL
+
+
+def test_attn_rejects_bad_args(device):
+    q = torch.zeros(1, 8, 1, 64, dtype=torch.bfloat16, device=device)
+    with pytest.raises(ValueError):
+        N.attn_fwd(q, q, q)

@@ -1,0 +1,119 @@
+"""DiT forward and sampling-loop parity: MI355X path vs the CPU oracle (oracle/dit.py, oracle/sampler.py).
+
+Both run the same seeded weights (reference init distributions, AdaLN output layers randomised so the
+modulation path is exercised) and inputs. The product computes every bf16 op with the reference's
+rounding points; remaining differences are fp32 accumulation order inside GEMMs/attention and the
+bf16 rounding of P in flash attention, which compound through the blocks.
+Tolerances (rel-L2 of the fp32 output): one DiT forward <= 1e-2; the tiny 3-step sampler trajectory
+<= 1e-2. Measured values are printed (pytest -s) and recorded in DESIGN.md.
+"""
+import dataclasses
+
+import pytest
+import torch
+
+from cosmos_predict2.dit import MinimalV1LVGDiT, init_state_dict
+from cosmos_predict2.model import Video2WorldModelRectifiedFlow
+from cosmos_predict2.net_config import SamplerConfig, tiny_dit
+from oracle import dit as odit
+from oracle import sampler as osamp
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_l2(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm()).item()
+
+
+def _setup(cfg, seed=0):
+    sd = init_state_dict(cfg, seed=seed, zero_adaln_out=False)
+    return sd, {"net." + k: v for k, v in sd.items()}
+
+
+@pytest.mark.parametrize("T,H,W,blocks", [(3, 16, 16, 2), (2, 8, 24, 1)])
+def test_dit_forward_matches_oracle(device, T, H, W, blocks):
+    cfg = tiny_dit(num_blocks=blocks)
+    sd, sd_ref = _setup(cfg)
+    g = torch.Generator().manual_seed(10)
+    x = torch.randn(1, 16, T, H, W, generator=g)
+    mask = torch.zeros(1, 1, T, H, W)
+    mask[:, :, :1] = 1
+    t = torch.tensor([[0.1] + [877.0] * (T - 1)])
+    ctx = torch.randn(1, 512, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
+    ref = odit.dit_forward(dataclasses.asdict(cfg), sd_ref, x, t, ctx, mask)
+    net = MinimalV1LVGDiT(cfg, device=device)
+    net.load_state_dict(sd_ref)
+    out = net(x.to(device).to(torch.bfloat16), t.to(device), ctx.to(device),
+              condition_video_input_mask_B_C_T_H_W=mask.to(device))
+    torch.cuda.synchronize()
+    err = rel_l2(out.cpu(), ref)
+    print(f"dit forward rel-L2 T={T} H={H} W={W} blocks={blocks}: {err:.3e}")
+    assert torch.isfinite(out).all()
+    assert err <= 1e-2, err
+
+
+def _sampler_case(device, guidance):
+    cfg = tiny_dit(num_blocks=2)
+    sd, sd_ref = _setup(cfg, seed=1)
+    T, H, W = 3, 16, 16
+    g = torch.Generator().manual_seed(20)
+    gt = torch.randn(1, 16, T, H, W, generator=g)
+    ctx_c = torch.randn(1, 512, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
+    ctx_u = torch.randn(1, 512, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
+    model = Video2WorldModelRectifiedFlow(cfg, SamplerConfig(use_kerras_sigma_at_inference=True,
+                                                             conditional_frame_timestep=0.1), device=device)
+    model.load_state_dict(sd_ref)
+    kw = dict(num_cond=1, guidance=guidance, seed=0, num_steps=2, use_karras=True, cond_frame_t=0.1)
+    ref = osamp.generate(dataclasses.asdict(cfg), sd_ref, gt, ctx_c, ctx_u, **kw)
+    out = model.sample_latents(gt.to(device), ctx_c.to(device), ctx_u.to(device), state_shape=(16, T, H, W),
+                               num_conditional_frames=1, guidance=guidance, seed=0, num_steps=2)
+    torch.cuda.synchronize()
+    return rel_l2(out.cpu(), ref)
+
+
+def _fake(xv, tv, b):
+    """Deterministic stand-in denoiser evaluated on the CPU (same bits on both paths)."""
+    return torch.sin(xv.float() * (1.0 + 0.25 * b) + tv)
+
+
+@pytest.mark.parametrize("num_steps,karras,cft", [(2, True, 0.1), (6, False, -1.0)])
+def test_sampler_plumbing_bit_exact(device, num_steps, karras, cft):
+    """Oracle loop vs fused CFG-batched loop with an identical fake denoiser: patchify, per-frame
+    timesteps, frame replacement, GT velocity, CFG and UniPC must agree bit for bit."""
+    cfg = tiny_dit()
+    T, H, W = 3, 8, 12
+    g = torch.Generator().manual_seed(21)
+    gt = torch.randn(1, 16, T, H, W, generator=g)
+    ctx_c = torch.zeros(1, 4, 8)
+    ctx_u = torch.ones(1, 4, 8)
+
+    def oracle_fn(c, s, x, t, ctx, mask):
+        b = 0 if ctx is ctx_c else 1
+        ts = (t.float() * cfg.timestep_scale)[0]  # [T]
+        return _fake(x, ts[None, None, :, None, None], b)
+
+    ref = osamp.generate(dataclasses.asdict(cfg), None, gt, ctx_c, ctx_u, num_cond=1, guidance=7.0, seed=3,
+                         num_steps=num_steps, use_karras=karras, cond_frame_t=cft, dit_fn=oracle_fn)
+
+    def device_fn(rows, t_B_T, geo):
+        r = rows.cpu()[:, 0, :64].view(-1, 16, 4).transpose(1, 2).reshape(-1, 64)  # (c p) -> (p c)
+        tok_t = torch.arange(geo.n_tok) // geo.hw
+        outs = [_fake(r, t_B_T.cpu()[b][tok_t][:, None], b) for b in range(2)]
+        return torch.stack(outs, 1).to(rows.device)
+
+    model = Video2WorldModelRectifiedFlow(cfg, SamplerConfig(use_kerras_sigma_at_inference=karras,
+                                                             conditional_frame_timestep=cft), device=device)
+    out = model.sample_latents(gt.to(device), ctx_c, ctx_u, state_shape=(16, T, H, W), num_conditional_frames=1,
+                               guidance=7.0, seed=3, num_steps=num_steps, net_fn=device_fn)
+    assert torch.equal(out.cpu(), ref)
+
+
+@pytest.mark.parametrize("guidance,tol", [(0.0, 1e-2), (7.0, 1e-1)])
+def test_sampler_matches_oracle(device, guidance, tol):
+    """End to end vs the oracle DiT. With guidance g the velocity is (1+g) c - g u; with random text
+    contexts c and u differ by only ~2.5 % (tools/diag_batch.py), so the per-branch bf16 error
+    (~1e-3 even between two device runs that only differ in GEMM tiling) is amplified ~(1+2g) = 15x:
+    hence 1e-1 at g = 7 and 1e-2 at g = 0. The plumbing itself is checked bit-exact above."""
+    err = _sampler_case(device, guidance)
+    print(f"sampler vs oracle (Karras 2 steps = 3 evals x CFG, g={guidance}) rel-L2: {err:.3e}")
+    assert err <= tol, err

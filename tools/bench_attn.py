@@ -1,0 +1,50 @@
+"""Micro-benchmark of cp25_attn_fwd at the DiT's shapes (timed with HIP events on the launch stream).
+
+usage: python tools/bench_attn.py [--L 109120] [--B 2] [--H 16] [--iters 5]
+Prints one JSON line per shape: ms per launch and TFLOP/s (4*B*H*Lq*Lk*D algorithmic FLOP).
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "cosmos-predict2.5_amd"))
+
+import torch  # noqa: E402
+
+from cosmos_predict2 import _native as N  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--L", type=int, default=109120)
+    ap.add_argument("--Lk", type=int, default=0)
+    ap.add_argument("--B", type=int, default=2)
+    ap.add_argument("--H", type=int, default=16)
+    ap.add_argument("--iters", type=int, default=5)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    Lk = a.Lk or a.L
+    g = torch.Generator(device=dev).manual_seed(0)
+    q = torch.randn(a.B, a.L, a.H, 128, device=dev, generator=g).to(torch.bfloat16)
+    k = torch.randn(a.B, Lk, a.H, 128, device=dev, generator=g).to(torch.bfloat16)
+    v = torch.randn(a.B, Lk, a.H, 128, device=dev, generator=g).to(torch.bfloat16)
+    o = N.attn_fwd(q, k, v)
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(a.iters):
+        N.attn_fwd(q, k, v, out=o)
+    e1.record(st)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / a.iters
+    flop = 4.0 * a.B * a.H * a.L * Lk * 128
+    print(json.dumps({"kernel": "attn_fwd", "B": a.B, "H": a.H, "Lq": a.L, "Lk": Lk, "ms": ms,
+                      "tflops": flop / ms / 1e9}))
+
+
+if __name__ == "__main__":
+    main()
