@@ -57,7 +57,9 @@ SIGNATURES = {
     "cp25_patchify": [_P, _P, _P, _P, _P, _I64, _I64, _I64, _P],
     "cp25_cfg_velocity": [_P, _I, _P, _P, _P, _F, _I, _P, _I64, _I64, _I64, _P],
     "cp25_unipc_step": [_P, _P, _P, _P, _P, _I64, ctypes.POINTER(UniPCParams), _P],
-    "cp25_conv3d": None,  # filled below (VAE)
+    "cp25_conv3d": [ctypes.POINTER(ctypes.c_void_p), _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I,
+                    _I, _I, _I, _I, _I, _I, _P],
+    "cp25_rms_norm_silu": [_P, _P, _P, _I64, _I, _I, _P],
 }
 
 
@@ -244,3 +246,32 @@ def unipc_step(x: torch.Tensor, v: torch.Tensor, m0: torch.Tensor, m1: torch.Ten
     rc = lib.cp25_unipc_step(_ptr(x), _ptr(v), _ptr(m0), _ptr(m1), _ptr(last), x.numel(), ctypes.byref(params),
                              _stream(x.device))
     _check("cp25_unipc_step", rc)
+
+
+# ----------------------------------------------------------------------------- VAE
+def conv3d(frames, weight: torch.Tensor, bias: Optional[torch.Tensor], out: torch.Tensor, *, Hin: int, Win: int,
+           Cin: int, Cout: int, Tout: int, KT: int, KH: int, KW: int, stride_t: int = 1, stride_hw: int = 1,
+           pad: tuple = (0, 0, 0, 0), upsample: bool = False, out_split: int = 0,
+           residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Implicit-GEMM causal conv (see include/cp25.h). frames: list of channels-last frame tensors
+    (or None for a zero frame); weight [Cout, KT, KH, KW, Cin] bf16; pad = (top, left, bottom, right)."""
+    lib = load_library()
+    ptrs = (ctypes.c_void_p * len(frames))(*[(_ptr(f) if f is not None else None) for f in frames])
+    dev = out.device
+    rc = lib.cp25_conv3d(ptrs, len(frames), _ptr(weight), _ptr(bias), _ptr(residual), _ptr(out), Hin, Win, Cin, Cout,
+                         Tout, KT, KH, KW, stride_t, stride_hw, pad[0], pad[1], pad[2], pad[3], int(upsample),
+                         out_split, _stream(dev))
+    _check("cp25_conv3d", rc)
+    return out
+
+
+def rms_norm_silu(x: torch.Tensor, gamma: torch.Tensor, silu: bool = True, out: Optional[torch.Tensor] = None):
+    lib = load_library()
+    C = x.shape[-1]
+    if out is None:
+        out = torch.empty_like(x)
+    if not x.is_contiguous():
+        raise ValueError("rms_norm_silu expects a contiguous channels-last tensor")
+    rc = lib.cp25_rms_norm_silu(_ptr(x), _ptr(gamma), _ptr(out), x.numel() // C, C, int(silu), _stream(x.device))
+    _check("cp25_rms_norm_silu", rc)
+    return out

@@ -110,6 +110,32 @@ typedef struct cp25_unipc_params {
 int cp25_unipc_step(float* x, const float* v, float* m0, float* m1, float* last, int64_t n,
                     const cp25_unipc_params* params, hipStream_t stream);
 
+/* ---------------------------------------------------------------- Wan2.1 VAE
+ * Activations are channels-last frames [H][W][C] bf16.
+ *
+ * cp25_conv3d: implicit-GEMM convolution out[to] = sum_{kt,kh,kw,ci} W[co][kt][kh][kw][ci] *
+ * in(frame to*stride_t + kt)[hi][wi][ci] + bias[co] (fp32 accumulation, bf16 output), then
+ * (if residual != NULL) out = out + residual (bf16 add). `frames` is a table of n_frames (<= 24)
+ * frame pointers [Hin][Win][Cin]; a NULL entry is a zero frame (causal padding). Spatial: pad_top /
+ * pad_left / pad_bottom / pad_right zeros, stride_hw; upsample=1 first nearest-upsamples the input 2x.
+ * out: [Tout][Ho][Wo][Cout]; with out_split = c > 0 (Cout == 2c) output channel co >= c goes to frame
+ * 2*to + 1, channel co - c (the upsample3d time_conv interleave), out being [2*Tout][Ho][Wo][c].
+ * Cin % 16 == 0 (pad channels on the host). Weight layout [Cout][KT][KH][KW][Cin] bf16.
+ * Replaces: CausalConv3d.forward (tokenizers/wan2pt1.py:44-62), Resample convs (:96-110, :133-145,
+ * :159), ResidualBlock shortcut + residual add (:204, :222), AttentionBlock to_qkv / proj (:236-261),
+ * WanVAE_ conv1 / conv2 (:494-495). */
+int cp25_conv3d(const void* const* frames, int n_frames, const void* weight, const void* bias, const void* residual,
+                void* out, int Hin, int Win, int Cin, int Cout, int Tout, int KT, int KH, int KW, int stride_t,
+                int stride_hw, int pad_top, int pad_left, int pad_bottom, int pad_right, int upsample, int out_split,
+                hipStream_t stream);
+
+/* y = F.normalize(x, dim=C) * sqrt(C) * gamma [then SiLU] per pixel of n_pix channels-last pixels,
+ * with the reference's bf16 rounding after each torch op. C % 32 == 0, C/32 in {1,2,3,6,12}.
+ * Replaces: RMS_norm.forward (+ nn.SiLU) in ResidualBlock / head / AttentionBlock (wan2pt1.py:65-77,
+ * :195-203, :235, :313-315, :413). */
+int cp25_rms_norm_silu(const void* x, const void* gamma, void* y, int64_t n_pix, int C, int do_silu,
+                       hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

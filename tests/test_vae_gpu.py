@@ -1,0 +1,116 @@
+"""Wan2.1 VAE parity: HIP implicit-GEMM conv path vs the CPU oracle (oracle/vae.py) on seeded weights.
+
+Single convolution: the kernel accumulates in fp32 like cuDNN; tolerance rel-L2 <= 2e-3 (bf16 output
+rounding + accumulation order). Full encode / decode stacks ~30 bf16 convolutions and norms; the
+tolerance is rel-L2 <= 2e-2 (bf16 rounding flips compound through the stack), measured values are
+printed and recorded in DESIGN.md.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from cosmos_predict2 import _native as N
+from cosmos_predict2.vae import Wan2pt1VAEInterface, _Conv, init_vae_state_dict
+from oracle import vae as ovae
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_l2(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm()).item()
+
+
+@pytest.mark.parametrize("cin,cout,k,stride,up", [(96, 96, 3, 1, False), (16, 384, 3, 1, False),
+                                                  (192, 96, 3, 1, True), (96, 96, 3, 2, False),
+                                                  (384, 1152, 1, 1, False), (96, 3, 3, 1, False)])
+def test_conv2d_like(device, cin, cout, k, stride, up):
+    g = torch.Generator().manual_seed(cin + cout)
+    H, W = 12, 20
+    x = torch.randn(1, cin, H, W, generator=g).to(torch.bfloat16)
+    w = (torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5).to(torch.bfloat16)
+    b = (0.1 * torch.randn(cout, generator=g)).to(torch.bfloat16)
+    xi = F.interpolate(x.float(), scale_factor=2.0, mode="nearest-exact") if up else x.float()
+    if stride == 2:
+        ref = F.conv2d(F.pad(xi, (0, 1, 0, 1)), w.float(), b.float(), stride=2)
+    else:
+        ref = F.conv2d(xi, w.float(), b.float(), padding=k // 2)
+    ref = ref.to(torch.bfloat16)
+    conv = _Conv(w, b, device)
+    xl = x[0].permute(1, 2, 0).contiguous().to(device)  # [H, W, C]
+    pad = (0, 0, 1, 1) if stride == 2 else (k // 2,) * 4
+    out = conv([xl], 1, H, W, stride_hw=stride, pad=pad, upsample=up)
+    err = rel_l2(out[0].permute(2, 0, 1).cpu(), ref[0])
+    assert err <= 2e-3, err
+
+
+def test_causal_conv3d_with_cache(device):
+    """3x3x3 causal conv over [cache(2 frames) | x(3 frames)] vs F.conv3d on the concatenated clip."""
+    g = torch.Generator().manual_seed(5)
+    C, H, W = 96, 10, 14
+    cache = torch.randn(1, C, 2, H, W, generator=g).to(torch.bfloat16)
+    x = torch.randn(1, C, 3, H, W, generator=g).to(torch.bfloat16)
+    w = (torch.randn(C, C, 3, 3, 3, generator=g) / (27 * C) ** 0.5).to(torch.bfloat16)
+    b = (0.1 * torch.randn(C, generator=g)).to(torch.bfloat16)
+    ref = F.conv3d(F.pad(torch.cat([cache, x], 2).float(), (1, 1, 1, 1, 0, 0)), w.float(), b.float()).to(torch.bfloat16)
+    conv = _Conv(w, b, device)
+    cl = cache[0].permute(1, 2, 3, 0).contiguous().to(device)
+    xl = x[0].permute(1, 2, 3, 0).contiguous().to(device)
+    out = conv([cl[0], cl[1], xl[0], xl[1], xl[2]], 3, H, W, pad=(1, 1, 1, 1))
+    assert rel_l2(out.permute(3, 0, 1, 2).cpu(), ref[0]) <= 2e-3
+
+
+def test_rms_norm_silu(device):
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(1, 192, 3, 5, 7, generator=g).to(torch.bfloat16)
+    gamma = (1 + 0.1 * torch.randn(192, 1, 1, 1, generator=g)).to(torch.bfloat16)
+    ref = ovae.silu(ovae.rms_norm(x, gamma))
+    out = N.rms_norm_silu(x[0].permute(1, 2, 3, 0).contiguous().to(device), gamma.reshape(-1).to(device))
+    o = out.permute(3, 0, 1, 2).cpu()
+    assert (o.float() - ref[0].float()).abs().max().item() <= 2 * 2 ** -7 * ref.float().abs().max().item()
+    assert (o == ref[0]).float().mean().item() >= 0.99
+
+
+@pytest.fixture(scope="module")
+def vae_pair():
+    sd = init_vae_state_dict(seed=0)
+    return sd
+
+
+def test_vae_encode_matches_oracle(device, vae_pair):
+    sd = vae_pair
+    g = torch.Generator().manual_seed(7)
+    video = (torch.rand(1, 3, 9, 64, 96, generator=g) * 2 - 1).to(torch.bfloat16)
+    ref = ovae.encode(sd, video, temporal_window=4)
+    tok = Wan2pt1VAEInterface(sd, device=device, temporal_window=4)
+    out = tok.encode(video.to(device))
+    torch.cuda.synchronize()
+    assert out.shape == ref.shape, (out.shape, ref.shape)
+    err = rel_l2(out.cpu(), ref)
+    print(f"vae encode rel-L2: {err:.3e}")
+    assert err <= 2e-2, err
+
+
+def test_vae_decode_matches_oracle(device, vae_pair):
+    sd = vae_pair
+    g = torch.Generator().manual_seed(8)
+    z = torch.randn(1, 16, 3, 8, 12, generator=g)
+    ref = ovae.decode(sd, z)
+    tok = Wan2pt1VAEInterface(sd, device=device)
+    out = tok.decode(z.to(device))
+    torch.cuda.synchronize()
+    assert out.shape == ref.shape, (out.shape, ref.shape)
+    err = rel_l2(out.cpu(), ref)
+    print(f"vae decode rel-L2: {err:.3e}")
+    assert err <= 2e-2, err
+
+
+def test_first_frame_encode_is_causal_prefix(device, vae_pair):
+    """Latent frame 0 depends only on pixel frame 0: encoding the 1-frame prefix reproduces it
+    bit-for-bit (this is what lets Image2World encode only the conditioning frame)."""
+    sd = vae_pair
+    g = torch.Generator().manual_seed(9)
+    video = (torch.rand(1, 3, 9, 64, 96, generator=g) * 2 - 1).to(torch.bfloat16).to(device)
+    tok = Wan2pt1VAEInterface(sd, device=device, temporal_window=4)
+    full = tok.encode(video)
+    first = tok.encode(video[:, :, :1])
+    assert torch.equal(full[:, :, :1], first)
