@@ -1,0 +1,158 @@
+"""Benchmark: frames/sec of Predict2.5-2B Image2World at 704x1280 x 121 frames, 35 UniPC steps.
+
+One step = one full Image2World video through the product API (Video2WorldInference.generate_vid2world):
+VAE encode of the conditioning frame, 35 Karras UniPC steps = 36 DiT evaluations x CFG 2 (cond and
+uncond batched, B = 2) on the 2B network at latent [16, 31, 88, 160] (L = 109 120 tokens), VAE decode
+of all 31 latent frames to 121 pixel frames. Synthetic data: seeded random weights with the 2B shapes,
+a random conditioning image, N(0, 1) text embeddings [1, 512, 100352]. bf16 compute.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+N > 1 (torchrun, one rank per GPU, RCCL): the video's token sequence is sharded context-parallel over
+the N ranks (K/V all-gather over xGMI); all ranks work on the same video (strong scaling).
+Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement").
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cosmos-predict2.5_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "frames/sec, Predict2.5-2B Image2World 720p×121f, 35 UniPC steps, CP=1/8"
+BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 MFMA
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1, help="timed videos")
+    ap.add_argument("--warmup", type=int, default=0, help="untimed videos before timing")
+    ap.add_argument("--num-steps", type=int, default=35, help="UniPC steps (35 = the metric)")
+    ap.add_argument("--frames", type=int, default=121)
+    ap.add_argument("--resolution", default="704,1280")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}: launch N>1 with torch.distributed.run")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from cosmos_predict2.pipeline import Video2WorldInference
+    from cosmos_predict2 import _native
+
+    _native.load_library()
+    h, w = (int(x) for x in a.resolution.split(","))
+    state_t = 1 + (a.frames - 1) // 4
+    pipe = Video2WorldInference("2B/post-trained", context_parallel_size=world, device=dev, state_t=state_t)
+    frames = pipe.model.tokenizer.get_pixel_num_frames(state_t)
+    # conditioning "image": frame 0 random uint8, later frames zero (read_and_process_image layout)
+    rng = np.random.RandomState(3)
+    vid = torch.zeros(1, 3, frames, h, w, dtype=torch.uint8)
+    vid[0, :, 0] = torch.from_numpy(rng.randint(0, 256, size=(3, h, w), dtype=np.uint8))
+    kw = dict(prompt="A robot arm pours coffee into a mug on a kitchen counter.", input_path=vid, guidance=7,
+              num_latent_conditional_frames=1, resolution=f"{h},{w}", seed=0, num_steps=a.num_steps)
+
+    # kernel-load prime (not a warmup step): one DiT evaluation + one latent frame decode
+    net = pipe.model.net
+    with torch.no_grad():
+        pipe.generate_vid2world(**dict(kw, num_steps=1)) if a.warmup == 0 else None
+    for _ in range(a.warmup):
+        pipe.generate_vid2world(**kw)
+
+    net.attn_events = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        video = pipe.generate_vid2world(**kw)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = tt.item()
+    assert video.shape[2] == frames and torch.isfinite(video).all()
+
+    # dominant kernel: self-attention flash kernel, HIP events around every launch in the timed region
+    ev = net.attn_events
+    net.attn_events = None
+    attn_ms = [e0.elapsed_time(e1) for e0, e1, _ in ev]
+    attn_flop = ev[0][2] if ev else 0.0
+    attn_avg_s = (sum(attn_ms) / len(attn_ms)) / 1e3 if attn_ms else float("nan")
+    achieved = attn_flop / attn_avg_s / 1e12 if attn_ms else 0.0
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        sys.path.insert(0, ROOT)
+        from oracle.cpu_baseline import dit_block_sample
+
+        cpu = dit_block_sample(L=state_t * (h // 16) * (w // 16), threads=a.cpu_threads)
+
+    if rank == 0:
+        ms = elapsed / a.steps * 1e3
+        valid = a.num_steps == 35 and a.frames == 121 and (h, w) == (704, 1280)
+        line = {
+            "metric": METRIC,
+            "value": frames * a.steps / elapsed,
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": ms,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic: seeded random 2B/VAE weights, random conditioning image, N(0,1) text embeddings",
+            "config": {
+                "workload": f"Predict2.5-2B Image2World {h}x{w}x{frames}f, {a.num_steps} Karras UniPC steps "
+                            f"({a.num_steps + 1} evals x CFG 2, batched), VAE encode cond frame + decode {frames}f",
+                "latent": [16, state_t, h // 8, w // 8],
+                "tokens": state_t * (h // 16) * (w // 16),
+                "global_batch": 1,
+                "parallelism": f"cp{world}",
+                "metric_config": valid,
+            },
+            "roofline": {
+                "bound": "mfma",
+                "kernel": "cp25_attn_fwd (DiT self-attention, bf16 MFMA)",
+                "achieved": achieved,
+                "peak": BF16_DENSE_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved / BF16_DENSE_PEAK_TFLOPS,
+                "traffic": None,
+                "launches_timed": len(attn_ms),
+                "avg_launch_ms": attn_avg_s * 1e3,
+                "flop_per_launch": attn_flop,
+            },
+            "phases_last_step_s": getattr(pipe, "last_timing", None),
+            "cpu_baseline": cpu and {k: cpu[k] for k in ("value", "unit", "cores", "kind", "sample")},
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -165,6 +165,8 @@ class MinimalV1LVGDiT:
         self.sd: Dict[str, torch.Tensor] = {}
         self._rope_cache: Dict[Tuple[int, int, int], Tuple[torch.Tensor, torch.Tensor]] = {}
         self.cp_group = None
+        # optional list collecting (start, end, flop) HIP events around every self-attention launch
+        self.attn_events: Optional[list] = None
 
     # ---------------------------------------------------------------- loading
     def load_state_dict(self, state_dict: Dict[str, torch.Tensor], strict: bool = True) -> None:
@@ -328,7 +330,14 @@ class MinimalV1LVGDiT:
                 kk = kv[:, :, :D].view(cp_size * n, B, H, hd).transpose(0, 1)
                 vv = kv[:, :, D:].view(cp_size * n, B, H, hd).transpose(0, 1)
             o = torch.empty((n, B, D), dtype=BF16, device=self.device)
+            if self.attn_events is not None:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
             N.attn_fwd(q, kk, vv, out=o.view(n, B, H, hd).transpose(0, 1), softmax_scale=scale_attn)
+            if self.attn_events is not None:
+                e1.record()
+                self.attn_events.append((e0, e1, 4.0 * B * H * n * kk.shape[1] * hd))
             y = F.linear(o.view(n * B, D), p[pre + "self_attn.output_proj.weight"])
             # ---- x += g_sa * y ; LN-mod for cross attention
             _, _, g_sa = mod(i, 0)

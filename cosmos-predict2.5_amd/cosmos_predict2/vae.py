@@ -25,6 +25,7 @@ from . import _native as N
 
 BF16 = torch.bfloat16
 CACHE_T = 2
+MAX_FRAMES = 24  # frame-table size of cp25_conv3d
 
 _MEAN = [-0.7571, -0.7089, -0.9113, 0.1075, -0.1745, 0.9653, -0.1517, 1.5508,
          0.4134, -0.0715, 0.5517, -0.3632, -0.1922, -0.9497, 0.2503, -0.2921]
@@ -155,9 +156,16 @@ class _Conv:
             out = torch.empty((2 * Tout, Ho, Wo, out_split), dtype=BF16, device=dev)
         else:
             out = torch.empty((Tout, Ho, Wo, self.cout), dtype=BF16, device=dev)
-        N.conv3d(frames, self.w, self.b, out, Hin=H, Win=W, Cin=self.cin_p, Cout=self.cout, Tout=Tout, KT=self.kt,
-                 KH=self.kh, KW=self.kw, stride_t=stride_t, stride_hw=stride_hw, pad=pad, upsample=upsample,
-                 out_split=out_split, residual=residual)
+        # the kernel takes at most MAX_FRAMES input frames per launch: chunk the output frames
+        per = max(1, (MAX_FRAMES - self.kt) // stride_t + 1)
+        f = 2 if out_split else 1
+        for t0 in range(0, Tout, per):
+            t1 = min(Tout, t0 + per)
+            fr = frames[t0 * stride_t: (t1 - 1) * stride_t + self.kt]
+            N.conv3d(fr, self.w, self.b, out[f * t0: f * t1], Hin=H, Win=W, Cin=self.cin_p, Cout=self.cout,
+                     Tout=t1 - t0, KT=self.kt, KH=self.kh, KW=self.kw, stride_t=stride_t, stride_hw=stride_hw,
+                     pad=pad, upsample=upsample, out_split=out_split,
+                     residual=None if residual is None else residual[f * t0: f * t1])
         return out
 
 
