@@ -12,14 +12,18 @@
 //     query on the lane), then O^T = V^T P^T, whose B operand is the S accumulator converted to bf16
 //     with no lane movement, and whose A operand (V^T) comes from ds_read_b64_tr_b16 (hardware
 //     transposed LDS read) of the row-major V tile;
-//   * one XOR swizzle of the 256-byte LDS rows serves both the ds_read_b128 row reads of K and the
-//     transposed reads of V without bank conflicts;
+//   * padded LDS rows (K 272 B, V 320 B) keep both the ds_read_b128 row reads of K and the transposed
+//     reads of V bank-conflict-free with every address a per-lane base + immediate; the tile loop is
+//     unrolled over the two LDS buffers so no address arithmetic remains in it;
+//   * the O rescale of the online softmax is skipped (exactly) when no row max of the wave grew;
 //   * grid remapped so the workgroups of one XCD share a (batch, head): their K/V stream hits in
 //     that XCD's L2 instead of HBM.
 // Numerics: scores and the running max/sum are fp32, P is rounded to bf16 before P.V (as every
 // flash-attention kernel the reference dispatches to does), O is accumulated in fp32, normalised
 // and rounded once to bf16.
 #include "cp25_common.h"
+
+#include <type_traits>
 
 namespace {
 
@@ -29,22 +33,26 @@ constexpr int kQRows = 32;     // query rows per wave
 constexpr int kQBlk = kWaves * kQRows;  // 256 query rows per workgroup
 constexpr int kKBlk = 64;      // keys per tile
 constexpr int kThreads = kWaves * 64;
-constexpr int kTileBytes = kKBlk * kD * 2;  // 16 KiB
-// LDS: [buf][K|V][64 rows][256 B]
-constexpr int kLdsBytes = 2 * 2 * kTileBytes;
-
-// 16-byte chunk swizzle inside a 256-byte row (cdna_hip_programming.md T10 image (b)).
-__device__ __forceinline__ int swz(int row, int ch) { return ch ^ (((row & 3) << 2) | ((row >> 2) & 3)); }
-__device__ __forceinline__ int lds_off(int row, int ch) { return row * 256 + 16 * swz(row, ch); }
+// LDS layout (bytes): [V0 | V1 | K0 | K1]. Padded rows instead of an XOR swizzle so every LDS read
+// is one per-lane base VGPR + a compile-time immediate (no per-tile address arithmetic):
+//   K rows 272 B (256 + 16): the 16 rows a ds_read_b128 lane group reads at one column land on 16
+//     distinct 16-B bank slots;
+//   V rows 320 B (256 + 64): the 4 rows x 64 B a half-wave of ds_read_b64_tr_b16 reads land on the
+//     4 distinct 64-B quarters of the 256-B bank row.
+constexpr int kKStride = 272;
+constexpr int kVStride = 320;
+constexpr int kVBuf = kKBlk * kVStride;  // 20480
+constexpr int kKBuf = kKBlk * kKStride;  // 17408
+constexpr int kV0 = 0, kV1 = kVBuf, kK0 = 2 * kVBuf, kK1 = 2 * kVBuf + kKBuf;
+constexpr int kLdsBytes = 2 * kVBuf + 2 * kKBuf;  // 75776
 
 typedef __attribute__((address_space(3))) s16x4* lds_s16x4_ptr;
 
-__device__ __forceinline__ bf16x8 tr_read_pair(const char* smem, int off_a, int off_b) {
-  s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_ptr)(smem + off_a));
-  s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_ptr)(smem + off_b));
-  s16x4 lo = a, hi = b;
+__device__ __forceinline__ bf16x8 tr_read_pair(const char* pa, const char* pb) {
+  s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_ptr)pa);
+  s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_ptr)pb);
   typedef short s16x8 __attribute__((ext_vector_type(8)));
-  s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  s16x8 r = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
   return __builtin_bit_cast(bf16x8, r);
 }
 
@@ -68,6 +76,7 @@ struct AttnArgs {
   float scale_log2; // softmax scale * log2(e)
 };
 
+template <int kKind>  // 0: self-attention, 1: cross-attention (separate symbols in profiles)
 __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
 
@@ -107,89 +116,87 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   const int ntiles = (a.Lk + kKBlk - 1) / kKBlk;
 
   // staging: each thread owns 2 K chunks and 2 V chunks (16 B each) of a 64x128 tile
+  const int srow0 = tid >> 4, sch = tid & 15;  // chunk i: row srow0 + 32 i
   u32x4 stK[2], stV[2];
-  auto stage_load = [&](int t) {
+  // branch-free staging loads: rows past the end are clamped to the last key (finite data; their
+  // scores are masked to -inf and their P is 0), tiles past the end re-load the last tile (unused)
+  auto load_rows = [&](const unsigned short* base, int64_t sl, int t, u32x4 (&dst)[2]) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int c = tid + kThreads * i;
-      const int row = c >> 4, ch = c & 15;
-      const int key = t * kKBlk + row;
-      if (key < a.Lk) {
-        stK[i] = *reinterpret_cast<const u32x4*>(kp + (int64_t)key * a.k_sl + ch * 8);
-        stV[i] = *reinterpret_cast<const u32x4*>(vp + (int64_t)key * a.v_sl + ch * 8);
-      } else {
-        stK[i] = u32x4{0u, 0u, 0u, 0u};
-        stV[i] = u32x4{0u, 0u, 0u, 0u};
-      }
+      const int key = min(t * kKBlk + srow0 + 32 * i, a.Lk - 1);
+      dst[i] = *reinterpret_cast<const u32x4*>(base + (int64_t)key * sl + sch * 8);
     }
   };
-  auto stage_write = [&](int buf) {
-    char* kb = smem + buf * 2 * kTileBytes;
-    char* vb = kb + kTileBytes;
+  char* const k_wr = smem + srow0 * kKStride + sch * 16;
+  char* const v_wr = smem + srow0 * kVStride + sch * 16;
+  auto write_k = [&](auto BUF) {
+    constexpr int kb = decltype(BUF)::value ? kK1 : kK0;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + kThreads * i;
-      const int row = c >> 4, ch = c & 15;
-      *reinterpret_cast<u32x4*>(kb + lds_off(row, ch)) = stK[i];
-      *reinterpret_cast<u32x4*>(vb + lds_off(row, ch)) = stV[i];
-    }
+    for (int i = 0; i < 2; ++i) *reinterpret_cast<u32x4*>(k_wr + kb + 32 * i * kKStride) = stK[i];
+  };
+  auto write_v = [&](auto BUF) {
+    constexpr int vb = decltype(BUF)::value ? kV1 : kV0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) *reinterpret_cast<u32x4*>(v_wr + vb + 32 * i * kVStride) = stV[i];
   };
 
-  stage_load(0);
-  stage_write(0);
-  __syncthreads();
-
-  // per-lane constant pieces of the V transposed-read address
-  const int grp = lane >> 4;        // 16-lane group
-  const int gi = lane & 15;         // index inside the group: 4q + p
+  // per-lane LDS read bases (everything else is an immediate offset)
+  const char* const k_rd = smem + l31 * kKStride + 16 * hl;  // + kt*32 rows + 32 s bytes
+  const int grp = lane >> 4, gi = lane & 15;
   const int tq = gi >> 2, tp = gi & 3;
-  const int trow_base = 4 * (grp >> 1) + tq;          // + 16*S (+8 for the second read)
-  const int tch_base = 2 * (grp & 1) + (tp >> 1);     // + 4*db
-  const int tbyte = 8 * (tp & 1);
+  const char* const v_rd = smem + (4 * (grp >> 1) + tq) * kVStride + 32 * (grp & 1) + 8 * tp;  // + rows, + 64 db
 
-  for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < ntiles) stage_load(t + 1);
+  // ragged last tile: its accumulator starts at -inf on keys >= Lk (masking folded into S's C operand)
+  const bool ragged = (a.Lk % kKBlk) != 0;
 
-    const char* kb = smem + buf * 2 * kTileBytes;
-    const char* vb = kb + kTileBytes;
-
-    // ---- S^T = K Q^T : two 32-key halves ----
-    f32x16 sacc[2];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sacc[kt][r] = 0.f;
-      const int krow = kt * 32 + l31;
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + lds_off(krow, 2 * s + hl));
-        sacc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[kt], 0, 0, 0);
-      }
-    }
-
-    // ---- mask the ragged last tile ----
-    if ((t + 1) * kKBlk > a.Lk) {
+  // S^T(tile in K buffer) = K Q^T. init: zeros, or -inf on keys >= Lk for the ragged last tile
+  // (masking folded into the MFMA's C operand)
+  auto qk_init = [&](int t, f32x16 (&S)[2]) {
+    if (ragged && t == ntiles - 1) {
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int key = t * kKBlk + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-          if (key >= a.Lk) sacc[kt][r] = -INFINITY;
+          S[kt][r] = key < a.Lk ? 0.f : -INFINITY;
         }
+    } else {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) S[kt][r] = 0.f;
     }
-
-    // ---- online softmax (lane-local: this lane + lane^32 hold one query row) ----
-    float mx = sacc[0][0];
+  };
+  auto qk_mma = [&](auto BUF, f32x16 (&S)[2]) {
+    constexpr int kb = decltype(BUF)::value ? kK1 : kK0;
 #pragma unroll
-    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sacc[0][r]);
+    for (int s = 0; s < 8; ++s)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[1][r]);
+      for (int kt = 0; kt < 2; ++kt) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(k_rd + kb + kt * 32 * kKStride + 32 * s);
+        S[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], S[kt], 0, 0, 0);
+      }
+  };
+  // online softmax, part 1: running max and (only if some row max grew: exact skip) the O rescale
+  auto sm_max = [&](f32x16 (&S)[2]) {
+    float mx = fmaxf(S[0][0], S[1][0]);
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(S[0][r], S[1][r]));
     mx = wave_swap_max(mx);
     const float m_new = fmaxf(m_run, mx * a.scale_log2);
-    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-    m_run = m_new;
-
+    if (__any(m_new > m_run)) {
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+      l_run *= alpha;
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+      m_run = m_new;
+    }
+  };
+  // part 2: P = exp2(S c - m) -> bf16 (lane-local B operand), row sum, O^T += V^T P^T
+  auto sm_pv = [&](auto BUF, f32x16 (&S)[2]) {
+    constexpr int vb = decltype(BUF)::value ? kV1 : kV0;
     bf16x8 pb[4];
     float psum = 0.f;
 #pragma unroll
@@ -199,33 +206,61 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
         bf16x8 v;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kt][8 * sp + j], a.scale_log2, -m_new));
+          const float p = __builtin_amdgcn_exp2f(fmaf(S[kt][8 * sp + j], a.scale_log2, -m_run));
           psum += p;
           v[j] = static_cast<__bf16>(p);
         }
         pb[2 * kt + sp] = v;
       }
-    l_run = l_run * alpha + psum;
+    l_run += psum;
 #pragma unroll
-    for (int d = 0; d < 4; ++d)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
-
-    // ---- O^T += V^T P^T ----
-#pragma unroll
-    for (int S = 0; S < 4; ++S) {
-      const int r0 = 16 * S + trow_base;
+    for (int Sx = 0; Sx < 4; ++Sx)
 #pragma unroll
       for (int db = 0; db < 4; ++db) {
-        const int ch = tch_base + 4 * db;
-        const int offa = r0 * 256 + 16 * swz(r0, ch) + tbyte;
-        const int offb = (r0 + 8) * 256 + 16 * swz(r0 + 8, ch) + tbyte;
-        bf16x8 vf = tr_read_pair(vb, offa, offb);
-        o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb[S], o[db], 0, 0, 0);
+        const char* pa = v_rd + vb + (16 * Sx) * kVStride + 64 * db;
+        const bf16x8 vf = tr_read_pair(pa, pa + 8 * kVStride);
+        o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb[Sx], o[db], 0, 0, 0);
       }
-    }
+  };
 
-    if (t + 1 < ntiles) stage_write(buf ^ 1);
+  // Software pipeline, K one tile ahead of V. Iteration t: QK^T of tile t+1 (K buffer (t+1)&1) is
+  // issued before the softmax + PV of tile t (V buffer t&1), so the matrix pipe stays busy while
+  // the VALU finishes the softmax. Registers prefetch K(t+2), V(t+1); after the compute they go to
+  // K buffer t&1 (K(t) was last read in iteration t-1) and V buffer (t+1)&1 (V(t-1), iteration t-1).
+  typedef std::integral_constant<int, 0> B0;
+  typedef std::integral_constant<int, 1> B1;
+  f32x16 SA[2], SB[2];
+  load_rows(kp, a.k_sl, 0, stK);
+  load_rows(vp, a.v_sl, 0, stV);
+  write_k(B0{});
+  write_v(B0{});
+  load_rows(kp, a.k_sl, 1, stK);
+  write_k(B1{});
+  __syncthreads();
+  qk_init(0, SA);
+  qk_mma(B0{}, SA);
+  __syncthreads();  // K buffer 0 is rewritten in iteration 0
+  for (int t = 0; t < ntiles; t += 2) {
+    // -- even tile t: scores SA, K(t+1) in buffer 1, V(t) in buffer 0
+    load_rows(kp, a.k_sl, t + 2, stK);
+    load_rows(vp, a.v_sl, t + 1, stV);
+    qk_init(t + 1, SB);
+    sm_max(SA);
+    qk_mma(B1{}, SB);
+    sm_pv(B0{}, SA);
+    write_k(B0{});
+    write_v(B1{});
+    __syncthreads();
+    if (t + 1 >= ntiles) break;
+    // -- odd tile t+1: scores SB, K(t+2) in buffer 0, V(t+1) in buffer 1
+    load_rows(kp, a.k_sl, t + 3, stK);
+    load_rows(vp, a.v_sl, t + 2, stV);
+    qk_init(t + 2, SA);
+    sm_max(SB);
+    qk_mma(B0{}, SA);
+    sm_pv(B1{}, SB);
+    write_k(B1{});
+    write_v(B0{});
     __syncthreads();
   }
 
@@ -273,7 +308,10 @@ extern "C" int cp25_attn_fwd(const void* q, const void* k, const void* v, void* 
   a.scale_log2 = softmax_scale * 1.4426950408889634f;
   const int64_t nwg = (int64_t)a.nqb * B * H;
   if (nwg > 0x7fffffff) return CP25_ERR_INVAL;
-  hipLaunchKernelGGL(attn_fwd_d128, dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
+  if (Lk <= 4096)
+    hipLaunchKernelGGL(attn_fwd_d128<1>, dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
+  else
+    hipLaunchKernelGGL(attn_fwd_d128<0>, dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
   CP25_LAUNCH_CHECK();
   return CP25_OK;
 }
