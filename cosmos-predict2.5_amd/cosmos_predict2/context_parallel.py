@@ -36,14 +36,27 @@ def split_tokens(x: torch.Tensor, group, dim: int = 0) -> torch.Tensor:
     return x.narrow(dim, tok0, n).contiguous()
 
 
+def all_gather_into(out: torch.Tensor, x: torch.Tensor, group) -> torch.Tensor:
+    """out[r*n:(r+1)*n] = rank r's x. RCCL (`nccl` backend) gathers straight between HBM buffers;
+    the gloo backend (CPU tests, or several ranks sharing one GPU in tests) stages through host memory."""
+    if dist.get_backend(group) == "gloo" and x.is_cuda:
+        w = dist.get_world_size(group)
+        xc = x.detach().contiguous().cpu()
+        parts = [torch.empty_like(xc) for _ in range(w)]
+        dist.all_gather(parts, xc, group=group)
+        out.copy_(torch.cat(parts, 0))
+        return out
+    dist.all_gather_into_tensor(out, x.contiguous(), group=group)
+    return out
+
+
 def gather_tokens(x: torch.Tensor, group) -> torch.Tensor:
     """Concatenate every rank's token shard along dim 0 (cat_outputs_cp on the token axis)."""
     r, w = cp_rank_world(group)
     if w == 1:
         return x
     out = torch.empty((w * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-    dist.all_gather_into_tensor(out, x.contiguous(), group=group)
-    return out
+    return all_gather_into(out, x, group)
 
 
 def broadcast(x: Optional[torch.Tensor], group, src_in_group: int = 0) -> Optional[torch.Tensor]:

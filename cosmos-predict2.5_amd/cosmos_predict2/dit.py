@@ -23,6 +23,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _native as N
+from .context_parallel import all_gather_into
 from .net_config import DiTConfig
 
 BF16 = torch.bfloat16
@@ -326,7 +327,7 @@ class MinimalV1LVGDiT:
                                     out2=kv_loc, out2_stride=2 * D)
                 N.copy_rows(qkv, 3 * D, kv_loc.view(n * B, 2 * D)[:, D:], 2 * D, n * B, D, src_offset=2 * D)
                 kv = torch.empty((cp_size * n, B, 2 * D), dtype=BF16, device=self.device)
-                torch.distributed.all_gather_into_tensor(kv, kv_loc, group=cp)
+                all_gather_into(kv, kv_loc, cp)  # RCCL over xGMI
                 kk = kv[:, :, :D].view(cp_size * n, B, H, hd).transpose(0, 1)
                 vv = kv[:, :, D:].view(cp_size * n, B, H, hd).transpose(0, 1)
             o = torch.empty((n, B, D), dtype=BF16, device=self.device)

@@ -76,10 +76,16 @@ def test_cp_token_sharding_world2():
 def test_token_range_rejects_uneven():
     from cosmos_predict2 import context_parallel as cpu
 
-    class G:  # minimal stand-in group for the divisibility check
-        pass
+    def world(r, w):  # cp_rank_world stand-in: the divisibility check needs only (rank, world)
+        return lambda group: (r, w)
 
-    with pytest.raises(ValueError):
-        # 109120 tokens split over 3 ranks is uneven
-        if 109120 % 3:
-            raise ValueError("uneven")
+    orig = cpu.cp_rank_world
+    try:
+        cpu.cp_rank_world = world(1, 3)
+        with pytest.raises(ValueError):
+            cpu.token_range(109120, object())  # 720p x 121f: 109120 tokens, not divisible by 3
+        for w in (1, 2, 4, 8):  # the CP sizes the bench runs all divide 109120
+            cpu.cp_rank_world = world(w - 1, w)
+            assert cpu.token_range(109120, object()) == ((w - 1) * (109120 // w), 109120 // w)
+    finally:
+        cpu.cp_rank_world = orig
