@@ -1,0 +1,79 @@
+"""Phase anatomy of the self-attention kernel from in-kernel s_memtime stamps (lab build).
+
+Build the instrumented library first (not part of the product):
+  hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -fno-honor-nans -DCP25_ATTN_PROBE -Iinclude \
+        -shared -o tools/lab/libattn_probe.so cosmos-predict2.5_amd/csrc/attn_fwd.hip
+usage: python tools/attn_probe.py [--L 32768] [--t0 200]
+Prints, per wave group, the mean cycles of each phase and barrier wait over 32 tiles x 8 workgroups.
+"""
+import argparse
+import ctypes
+import json
+import os
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--L", type=int, default=32768)
+    ap.add_argument("--B", type=int, default=2)
+    ap.add_argument("--H", type=int, default=16)
+    ap.add_argument("--t0", type=int, default=200)
+    ap.add_argument("--lib", default=os.path.join(ROOT, "tools", "lab", "libattn_probe.so"))
+    a = ap.parse_args()
+    lib = ctypes.CDLL(a.lib)
+    P = ctypes.c_void_p
+    lib.cp25_attn_fwd.argtypes = [P, P, P, P] + [ctypes.c_int] * 5 + [P] * 4 + [ctypes.c_float, P]
+    lib.cp25_attn_fwd.restype = ctypes.c_int
+    lib.cp25_attn_probe_set.argtypes = [P, ctypes.c_int]
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(0)
+    q, k, v = (torch.randn(a.B, a.L, a.H, 128, device=dev, generator=g).to(torch.bfloat16) for _ in range(3))
+    o = torch.empty_like(q)
+    probe = torch.zeros(8 * 8 * 32 * 4, dtype=torch.int64, device=dev)
+
+    def strides(t):
+        return (ctypes.c_int64 * 3)(t.stride(0), t.stride(1), t.stride(2))
+
+    st = [strides(t) for t in (q, k, v, o)]
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def run():
+        rc = lib.cp25_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), a.B, a.H, a.L, a.L, 128,
+                               *[ctypes.cast(s, P) for s in st], 128 ** -0.5, stream)
+        assert rc == 0, rc
+
+    lib.cp25_attn_probe_set(None, 0)
+    run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    run()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1)
+    lib.cp25_attn_probe_set(ctypes.c_void_p(probe.data_ptr()), a.t0)
+    run()
+    torch.cuda.synchronize()
+    T = probe.cpu().numpy().astype(np.int64).reshape(8, 8, 32, 4)  # wg, wave, tile, stamp
+    res = {"L": a.L, "ms": ms, "tflops": 4 * a.B * a.H * a.L * a.L * 128 / ms / 1e9}
+    for name, waves in (("A", range(0, 4)), ("B", range(4, 8))):
+        t = T[:, list(waves)]
+        d = {
+            "period": np.diff(t[..., 3], axis=2).mean(),
+            "ph1": (t[:, :, 1:, 0] - t[:, :, :-1, 3]).mean(),
+            "bar1": (t[..., 1] - t[..., 0]).mean(),
+            "ph2": (t[..., 2] - t[..., 1]).mean(),
+            "bar2": (t[..., 3] - t[..., 2]).mean(),
+        }
+        res[name] = {k: round(float(x), 1) for k, x in d.items()}
+    res["note"] = "A: ph1 = MFMA phase, ph2 = softmax; B: ph1 = softmax, ph2 = MFMA (cycles of s_memtime)"
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
