@@ -150,6 +150,20 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
 
 
 # ----------------------------------------------------------------------------- DiT elementwise
+def _check_frames(mod: torch.Tensor, *, n_tok: int, B: int, tok0: int, hw: int) -> None:
+    """The kernels index modulation rows by frame (tok // hw) and batch: both must be in range."""
+    if mod.dim() != 3 or mod.shape[0] < B or hw <= 0 or tok0 < 0 or n_tok < 0:
+        raise ValueError(f"modulation {tuple(mod.shape)} does not cover B={B}")
+    if n_tok and (tok0 + n_tok - 1) // hw >= mod.shape[1]:
+        raise ValueError(f"tokens [{tok0}, {tok0 + n_tok}) reach frame {(tok0 + n_tok - 1) // hw}, "
+                         f"but the modulation has {mod.shape[1]} frames")
+
+
+def _check_mask(frame_mask: torch.Tensor, *, n_tok: int, tok0: int, hw: int) -> None:
+    if hw <= 0 or tok0 < 0 or (n_tok and (tok0 + n_tok - 1) // hw >= frame_mask.numel()):
+        raise ValueError(f"tokens [{tok0}, {tok0 + n_tok}) with hw={hw} exceed the {frame_mask.numel()}-frame mask")
+
+
 def ln_mod(x: torch.Tensor, shift: torch.Tensor, scale: torch.Tensor, *, n_tok: int, B: int, tok0: int, hw: int,
            x_st: int, x_sb: int, y: Optional[torch.Tensor] = None, gate: Optional[torch.Tensor] = None,
            x_out: Optional[torch.Tensor] = None, h_out: Optional[torch.Tensor] = None,
@@ -158,6 +172,7 @@ def ln_mod(x: torch.Tensor, shift: torch.Tensor, scale: torch.Tensor, *, n_tok: 
     shift/scale/gate are bf16 views [B, T, D] (strides (sb, st, 1), shared by all three)."""
     lib = load_library()
     D = shift.shape[-1]
+    _check_frames(shift, n_tok=n_tok, B=B, tok0=tok0, hw=hw)
     if h_out is None:
         h_out = torch.empty((n_tok, B, D), dtype=torch.bfloat16, device=x.device)
     if shift.stride() != scale.stride() or (gate is not None and gate.stride() != shift.stride()):
@@ -175,6 +190,9 @@ def final_ln_mod(x: torch.Tensor, shift: torch.Tensor, scale: torch.Tensor, *, n
                  eps: float = 1e-6) -> torch.Tensor:
     lib = load_library()
     D = shift.shape[-1]
+    _check_frames(shift, n_tok=n_tok, B=B, tok0=tok0, hw=hw)
+    if gate is not None:
+        _check_frames(gate, n_tok=n_tok, B=B, tok0=tok0, hw=hw)
     out = torch.empty((n_tok, B, D), dtype=torch.float32, device=x.device)
     gsb, gst = (gate.stride(0), gate.stride(1)) if gate is not None else (0, 0)
     if shift.stride() != scale.stride():
@@ -218,6 +236,7 @@ def patchify(xs: torch.Tensor, gt: Optional[torch.Tensor], frame_mask: torch.Ten
              pad_mask: Optional[torch.Tensor], *, tok0: int, hw: int) -> torch.Tensor:
     lib = load_library()
     n_tok = xs.shape[0]
+    _check_mask(frame_mask, n_tok=n_tok, tok0=tok0, hw=hw)
     out = torch.empty((n_tok, 72), dtype=torch.bfloat16, device=xs.device)
     rc = lib.cp25_patchify(_ptr(xs), _ptr(gt), _ptr(frame_mask), _ptr(pad_mask), _ptr(out), n_tok, tok0, hw,
                            _stream(xs.device))
@@ -230,6 +249,8 @@ def cfg_velocity(net: torch.Tensor, noise: Optional[torch.Tensor], gt: Optional[
                  hw: int) -> torch.Tensor:
     lib = load_library()
     n_tok, B, _ = net.shape
+    if frame_mask is not None:
+        _check_mask(frame_mask, n_tok=n_tok, tok0=tok0, hw=hw)
     out = torch.empty((n_tok, 64), dtype=torch.float32, device=net.device)
     rc = lib.cp25_cfg_velocity(_ptr(net), B, _ptr(noise), _ptr(gt), _ptr(frame_mask), float(guidance), int(cfg_mode),
                                _ptr(out), n_tok, tok0, hw, _stream(net.device))

@@ -6,18 +6,22 @@
 //
 // Design (MI355X-first, see DESIGN.md "attn_fwd"):
 //   * one workgroup = 8 waves = 256 query rows of one (batch, head); every wave owns 32 query rows;
-//   * K/V stream through LDS in 64-key tiles, double buffered, register-staged (issue global loads
-//     before the MFMA work on the current tile, write LDS after it), ONE barrier per tile;
 //   * "swapped" products so the softmax is lane-local: S^T = K Q^T (v_mfma_f32_32x32x16_bf16, the
 //     query on the lane), then O^T = V^T P^T, whose B operand is the S accumulator converted to bf16
 //     with no lane movement, and whose A operand (V^T) comes from ds_read_b64_tr_b16 (hardware
 //     transposed LDS read) of the row-major V tile;
+//   * ping-pong between the two waves of each SIMD (comment above attn_fwd_d128): one runs its 32
+//     MFMAs of a tile while the other runs its softmax, swapping at every barrier;
+//   * the MFMA phase's LDS operand reads are issued four MFMAs ahead (inline asm, counted lgkmcnt);
+//   * K/V stream through LDS in 64-key tiles, double buffered, register-staged by buffer_load with
+//     a wave-uniform descriptor (the hardware range check zero-fills rows past the end);
 //   * padded LDS rows (K 272 B, V 320 B) keep both the ds_read_b128 row reads of K and the transposed
-//     reads of V bank-conflict-free with every address a per-lane base + immediate; the tile loop is
-//     unrolled over the two LDS buffers so no address arithmetic remains in it;
+//     reads of V bank-conflict-free with every address a per-lane base + immediate;
 //   * the O rescale of the online softmax is skipped (exactly) when no row max of the wave grew;
 //   * grid remapped so the workgroups of one XCD share a (batch, head): their K/V stream hits in
 //     that XCD's L2 instead of HBM.
+// NaN inputs are not supported (built with -fno-honor-nans; the reference's flash kernels do not
+// define NaN propagation either).
 // Numerics: scores and the running max/sum are fp32, P is rounded to bf16 before P.V (as every
 // flash-attention kernel the reference dispatches to does), O is accumulated in fp32, normalised
 // and rounded once to bf16.
@@ -33,7 +37,7 @@ constexpr int kQRows = 32;     // query rows per wave
 constexpr int kQBlk = kWaves * kQRows;  // 256 query rows per workgroup
 constexpr int kKBlk = 64;      // keys per tile
 constexpr int kThreads = kWaves * 64;
-// LDS layout (bytes): [V0 | V1 | K0 | K1]. Padded rows instead of an XOR swizzle so every LDS read
+// LDS layout (bytes): [K0 | K1 | V0 | V1]. Padded rows instead of an XOR swizzle so every LDS read
 // is one per-lane base VGPR + a compile-time immediate (no per-tile address arithmetic):
 //   K rows 272 B (256 + 16): the 16 rows a ds_read_b128 lane group reads at one column land on 16
 //     distinct 16-B bank slots;
@@ -43,17 +47,19 @@ constexpr int kKStride = 272;
 constexpr int kVStride = 320;
 constexpr int kVBuf = kKBlk * kVStride;  // 20480
 constexpr int kKBuf = kKBlk * kKStride;  // 17408
-constexpr int kV0 = 0, kV1 = kVBuf, kK0 = 2 * kVBuf, kK1 = 2 * kVBuf + kKBuf;
+constexpr int kK0 = 0, kK1 = kKBuf, kV0 = 2 * kKBuf, kV1 = 2 * kKBuf + kVBuf;
 constexpr int kLdsBytes = 2 * kVBuf + 2 * kKBuf;  // 75776
 
 typedef __attribute__((address_space(3))) s16x4* lds_s16x4_ptr;
+typedef __attribute__((address_space(3))) const char* lds_char_ptr;
 
-__device__ __forceinline__ bf16x8 tr_read_pair(const char* pa, const char* pb) {
-  s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_ptr)pa);
-  s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_ptr)pb);
-  typedef short s16x8 __attribute__((ext_vector_type(8)));
-  s16x8 r = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-  return __builtin_bit_cast(bf16x8, r);
+// compile-time loop: f(integral_constant<int, I>) for I = 0 .. N-1, in order
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
 }
 
 __device__ __forceinline__ float wave_swap_max(float x) {
@@ -74,8 +80,37 @@ struct AttnArgs {
   int B, H, Lq, Lk;
   int nqb;          // query blocks per (b, h)
   float scale_log2; // softmax scale * log2(e)
+#ifdef CP25_ATTN_PROBE
+  unsigned long long* probe;  // [wg < 8][wave][tile - probe_t0 < 32][4] s_memtime stamps (lab build only)
+  int probe_t0;
+#endif
 };
 
+// Lab-build instrumentation (tools/attn_probe.py): s_memtime around the two barriers of a tile
+// iteration for the first 8 workgroups; compiled out of the product library.
+#ifdef CP25_ATTN_PROBE
+#define ATTN_STAMP(t, k)                                                                              \
+  do {                                                                                                \
+    const int pt_ = (t) - a.probe_t0;                                                                 \
+    if (a.probe && blockIdx.x < 8 && pt_ >= 0 && pt_ < 32)                                                 \
+      a.probe[(((size_t)blockIdx.x * kWaves + wave) * 32 + pt_) * 4 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define ATTN_STAMP(t, k) do { } while (0)
+#endif
+
+// Ping-pong schedule. Waves w and w+4 share a SIMD; the workgroup's waves split into group A
+// (waves 0-3) and group B (waves 4-7) that run opposite phases between the same barriers:
+//
+//   phase 2t  : A  MFMA  S = K(t+1) Q^T,  O^T += V(t)^T P(t)^T        B  softmax S(t) -> P(t), stage K
+//   phase 2t+1: A  softmax S(t+1) -> P(t+1), stage V                  B  MFMA (same products as A's)
+//
+// so every SIMD has one wave feeding the matrix pipe (32 back-to-back MFMAs) while its partner runs
+// the exp/max/sum VALU work in the issue slots the MFMAs leave free. K/V tiles are double buffered in
+// LDS; group B stages K (register-staged, loads issued two phases before their LDS write), group A
+// stages V. Buffer lifetimes: K(j) and V(j) live in buffer j&1; K(t+1), V(t) are read in phases 2t
+// and 2t+1; K(t+2) is written in phase 2t over K(t) (last read in 2t-1), V(t+1) in phase 2t+1 over
+// V(t-1) (last read in 2t-1).
 template <int kKind>  // 0: self-attention, 1: cross-attention (separate symbols in profiles)
 __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
@@ -90,6 +125,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   const int wave = tid >> 6;
   const int l31 = lane & 31;
   const int hl = lane >> 5;  // lane half
+  const bool group_b = __builtin_amdgcn_readfirstlane(tid) >= kThreads / 2;
 
   const unsigned short* qp = a.q + b * a.q_sb + h * a.q_sh;
   const unsigned short* kp = a.k + b * a.k_sb + h * a.k_sh;
@@ -115,74 +151,85 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
 
   const int ntiles = (a.Lk + kKBlk - 1) / kKBlk;
 
-  // staging: each thread owns 2 K chunks and 2 V chunks (16 B each) of a 64x128 tile
-  const int srow0 = tid >> 4, sch = tid & 15;  // chunk i: row srow0 + 32 i
-  u32x4 stK[2], stV[2];
-  // branch-free staging loads: rows past the end are clamped to the last key (finite data; their
-  // scores are masked to -inf and their P is 0), tiles past the end re-load the last tile (unused)
-  auto load_rows = [&](const unsigned short* base, int64_t sl, int t, u32x4 (&dst)[2]) {
+  // staging: a group's 256 threads own 4 chunks (16 B) each of a 64x128 tile: rows u/16 + 16 i,
+  // chunk u%16. buffer_load: the tile base is a wave-uniform descriptor (SALU only), the per-lane
+  // offset is loop-invariant, rows past Lk fall outside the descriptor's range and read as zero
+  // (their scores are masked to -inf).
+  const int u = tid & (kThreads / 2 - 1);
+  const int srow = u >> 4, sch = u & 15;
+  const int64_t sl = group_b ? a.k_sl : a.v_sl;
+  const unsigned short* sbase = group_b ? kp : vp;
+  const int st_off = (int)(srow * sl * 2) + sch * 16, st_step = (int)(16 * sl * 2);
+  u32x4 st[4];
+  auto load_tile = [&](int t) __attribute__((always_inline)) {
+    const int rows = min(a.Lk - t * kKBlk, kKBlk);
+    const int nbytes = rows > 0 ? (int)((rows - 1) * sl * 2) + 2 * kD : 0;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(sbase + (int64_t)t * kKBlk * sl), (short)0, nbytes,
+                                                        0x00020000);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int key = min(t * kKBlk + srow0 + 32 * i, a.Lk - 1);
-      dst[i] = *reinterpret_cast<const u32x4*>(base + (int64_t)key * sl + sch * 8);
-    }
+    for (int i = 0; i < 4; ++i)
+      st[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, st_off + i * st_step, 0, 0));
   };
-  char* const k_wr = smem + srow0 * kKStride + sch * 16;
-  char* const v_wr = smem + srow0 * kVStride + sch * 16;
-  auto write_k = [&](auto BUF) {
+  char* const k_wr = smem + srow * kKStride + sch * 16;
+  char* const v_wr = smem + srow * kVStride + sch * 16;
+  auto write_k = [&](auto BUF) __attribute__((always_inline)) {
     constexpr int kb = decltype(BUF)::value ? kK1 : kK0;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) *reinterpret_cast<u32x4*>(k_wr + kb + 32 * i * kKStride) = stK[i];
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(k_wr + kb + 16 * i * kKStride) = st[i];
   };
-  auto write_v = [&](auto BUF) {
+  auto write_v = [&](auto BUF) __attribute__((always_inline)) {
     constexpr int vb = decltype(BUF)::value ? kV1 : kV0;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) *reinterpret_cast<u32x4*>(v_wr + vb + 32 * i * kVStride) = stV[i];
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(v_wr + vb + 16 * i * kVStride) = st[i];
   };
 
   // per-lane LDS read bases (everything else is an immediate offset)
   const char* const k_rd = smem + l31 * kKStride + 16 * hl;  // + kt*32 rows + 32 s bytes
   const int grp = lane >> 4, gi = lane & 15;
   const int tq = gi >> 2, tp = gi & 3;
-  const char* const v_rd = smem + (4 * (grp >> 1) + tq) * kVStride + 32 * (grp & 1) + 8 * tp;  // + rows, + 64 db
+  const char* const v_rd = smem + kV0 + (4 * (grp >> 1) + tq) * kVStride + 32 * (grp & 1) + 8 * tp;  // + rows, + 64 db
+  // the same bases as 32-bit LDS addresses for the MFMA phase's asm reads (all offsets < 64 KiB)
+  const unsigned k_rd_lds = (unsigned)(uintptr_t)(lds_char_ptr)k_rd;
+  const unsigned v_rd_lds = (unsigned)(uintptr_t)(lds_char_ptr)v_rd;
 
-  // ragged last tile: its accumulator starts at -inf on keys >= Lk (masking folded into S's C operand)
-  const bool ragged = (a.Lk % kKBlk) != 0;
+  // ragged last tile: keys >= Lk get a -inf score (a uniform branch taken on that tile only)
+  const int ragged_tile = (a.Lk % kKBlk) != 0 ? a.Lk / kKBlk : -1;
 
-  // S^T(tile in K buffer) = K Q^T. init: zeros, or -inf on keys >= Lk for the ragged last tile
-  // (masking folded into the MFMA's C operand)
-  auto qk_init = [&](int t, f32x16 (&S)[2]) {
-    if (ragged && t == ntiles - 1) {
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = t * kKBlk + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-          S[kt][r] = key < a.Lk ? 0.f : -INFINITY;
-        }
-    } else {
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) S[kt][r] = 0.f;
-    }
-  };
-  auto qk_mma = [&](auto BUF, f32x16 (&S)[2]) {
+  f32x16 S[2];   // S^T of the tile awaiting its softmax
+  bf16x8 pb[4];  // P^T of the tile awaiting its P.V
+  const f32x16 zero16 = {};
+
+  // S^T = K Q^T on the K buffer; the first MFMA of each chain takes an inline-constant zero C
+  auto qk_mma = [&](auto BUF) __attribute__((always_inline)) {
     constexpr int kb = decltype(BUF)::value ? kK1 : kK0;
 #pragma unroll
     for (int s = 0; s < 8; ++s)
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         const bf16x8 kf = *reinterpret_cast<const bf16x8*>(k_rd + kb + kt * 32 * kKStride + 32 * s);
-        S[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], S[kt], 0, 0, 0);
+        S[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], s == 0 ? zero16 : S[kt], 0, 0, 0);
       }
   };
-  // online softmax, part 1: running max and (only if some row max grew: exact skip) the O rescale
-  auto sm_max = [&](f32x16 (&S)[2]) {
-    float mx = fmaxf(S[0][0], S[1][0]);
+  // online softmax of tile t: running max (O rescale skipped exactly when no row max of the wave
+  // grew), P = exp2(S c - m) -> bf16 (lane-local B operand of P.V), row sum
+  auto softmax = [&](int t) __attribute__((always_inline)) {
+    if (__builtin_expect(t == ragged_tile, 0)) {
 #pragma unroll
-    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(S[0][r], S[1][r]));
-    mx = wave_swap_max(mx);
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = t * kKBlk + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+          if (key >= a.Lk) S[kt][r] = -INFINITY;
+        }
+    }
+    // four independent v_max3 chains (this file builds with -fno-honor-nans: no canonicalising
+    // v_max before each fmaxf of an MFMA result)
+    float mc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) mc[j] = fmaxf(S[0][j], S[1][j]);
+#pragma unroll
+    for (int r = 4; r < 16; ++r) mc[r & 3] = fmaxf(fmaxf(mc[r & 3], S[0][r]), S[1][r]);
+    const float mx = wave_swap_max(fmaxf(fmaxf(fmaxf(mc[0], mc[1]), mc[2]), mc[3]));
     const float m_new = fmaxf(m_run, mx * a.scale_log2);
     if (__any(m_new > m_run)) {
       const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
@@ -193,11 +240,6 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
         for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
       m_run = m_new;
     }
-  };
-  // part 2: P = exp2(S c - m) -> bf16 (lane-local B operand), row sum, O^T += V^T P^T
-  auto sm_pv = [&](auto BUF, f32x16 (&S)[2]) {
-    constexpr int vb = decltype(BUF)::value ? kV1 : kV0;
-    bf16x8 pb[4];
     float psum = 0.f;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
@@ -213,55 +255,117 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
         pb[2 * kt + sp] = v;
       }
     l_run += psum;
-#pragma unroll
-    for (int Sx = 0; Sx < 4; ++Sx)
-#pragma unroll
-      for (int db = 0; db < 4; ++db) {
-        const char* pa = v_rd + vb + (16 * Sx) * kVStride + 64 * db;
-        const bf16x8 vf = tr_read_pair(pa, pa + 8 * kVStride);
-        o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb[Sx], o[db], 0, 0, 0);
-      }
+    // keep the whole softmax in this phase: s_barrier orders memory only, and without this the
+    // compiler sinks the exp/cvt work across it into the MFMA phase that consumes P
+    asm volatile("" ::"v"(pb[0]), "v"(pb[1]), "v"(pb[2]), "v"(pb[3]), "v"(l_run));
   };
 
-  // Software pipeline, K one tile ahead of V. Iteration t: QK^T of tile t+1 (K buffer (t+1)&1) is
-  // issued before the softmax + PV of tile t (V buffer t&1), so the matrix pipe stays busy while
-  // the VALU finishes the softmax. Registers prefetch K(t+2), V(t+1); after the compute they go to
-  // K buffer t&1 (K(t) was last read in iteration t-1) and V buffer (t+1)&1 (V(t-1), iteration t-1).
   typedef std::integral_constant<int, 0> B0;
   typedef std::integral_constant<int, 1> B1;
-  f32x16 SA[2], SB[2];
-  load_rows(kp, a.k_sl, 0, stK);
-  load_rows(vp, a.v_sl, 0, stV);
-  write_k(B0{});
-  write_v(B0{});
-  load_rows(kp, a.k_sl, 1, stK);
-  write_k(B1{});
-  __syncthreads();
-  qk_init(0, SA);
-  qk_mma(B0{}, SA);
-  __syncthreads();  // K buffer 0 is rewritten in iteration 0
-  for (int t = 0; t < ntiles; t += 2) {
-    // -- even tile t: scores SA, K(t+1) in buffer 1, V(t) in buffer 0
-    load_rows(kp, a.k_sl, t + 2, stK);
-    load_rows(vp, a.v_sl, t + 1, stV);
-    qk_init(t + 1, SB);
-    sm_max(SA);
-    qk_mma(B1{}, SB);
-    sm_pv(B0{}, SA);
-    write_k(B0{});
-    write_v(B1{});
-    __syncthreads();
-    if (t + 1 >= ntiles) break;
-    // -- odd tile t+1: scores SB, K(t+2) in buffer 0, V(t+1) in buffer 1
-    load_rows(kp, a.k_sl, t + 3, stK);
-    load_rows(vp, a.v_sl, t + 2, stV);
-    qk_init(t + 2, SA);
-    sm_max(SB);
-    qk_mma(B0{}, SA);
-    sm_pv(B1{}, SB);
+
+  // ---- prologue: K(0), V(0) -> buffer 0; K(1) -> buffer 1; S(0) for everyone, P(0) for A ----
+  load_tile(0);
+  if (group_b) write_k(B0{}); else write_v(B0{});
+  if (group_b) {
+    load_tile(1);
     write_k(B1{});
-    write_v(B0{});
-    __syncthreads();
+    load_tile(2);  // written in phase 0
+  } else {
+    load_tile(1);  // written in phase 1
+  }
+  __syncthreads();
+  qk_mma(B0{});
+  if (!group_b) softmax(0);
+  __syncthreads();
+
+  // one MFMA phase: QK^T of tile t+1 (if any) and P.V of tile t; t's parity picks the buffers
+  // (the QK^T after the last tile reads a stale K buffer; its scores are never used).
+  // MFMA j = 0..15: S[j&1] += K(rows 32(j&1)..) Q^T step j>>1 (one ds_read_b128 operand);
+  // MFMA j = 16..31: O^T[d block (j-16)&3] += V^T P^T step (j-16)>>2 (two ds_read_b64_tr_b16).
+  // The operand reads are inline asm issued four MFMAs ahead into a 5-deep register ring, each MFMA
+  // preceded by a counted lgkmcnt wait that names its operand ("+v": no use before the data lands).
+  // Nothing else touches LGKM in this phase (the barrier before it drained LDS and SMEM).
+  auto mfma_phase = [&](auto PAR) __attribute__((always_inline)) {
+    constexpr int par = decltype(PAR)::value;
+    constexpr int kb = (par ^ 1) ? kK1 : kK0;  // K(t+1)
+    constexpr int vb = par ? kVBuf : 0;         // V(t), relative to V0
+    bf16x8 ring[5];
+    auto issue = [&](auto JC) __attribute__((always_inline)) {
+      constexpr int j = decltype(JC)::value;
+      if constexpr (j < 16) {
+        constexpr int off = kb + (j & 1) * 32 * kKStride + 32 * (j >> 1);
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ring[j % 5]) : "v"(k_rd_lds), "i"(off));
+      } else if constexpr (j < 32) {
+        constexpr int off = vb + 16 * ((j - 16) >> 2) * kVStride + 64 * ((j - 16) & 3);
+        s16x4 lo, hi;
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(v_rd_lds), "i"(off));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(v_rd_lds), "i"(off + 8 * kVStride));
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        ring[j % 5] = __builtin_bit_cast(bf16x8, r);
+      }
+    };
+    constexpr auto nreads = [](int j) constexpr { return j < 16 ? 1 : (j < 32 ? 2 : 0); };
+    // the MFMA-phase wave outranks its softmax partner in issue arbitration (+8% measured)
+    __builtin_amdgcn_s_setprio(1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the counted waits below assume an empty LGKM queue
+    static_for<4>(issue);
+    static_for<32>([&](auto JC) __attribute__((always_inline)) {
+      constexpr int j = decltype(JC)::value;
+      issue(std::integral_constant<int, j + 4>{});
+      constexpr int pending = nreads(j + 1) + nreads(j + 2) + nreads(j + 3) + nreads(j + 4);
+      asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(ring[j % 5]) : "i"(pending));
+      if constexpr (j < 16) {
+        S[j & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ring[j % 5], qf[j >> 1], j < 2 ? zero16 : S[j & 1], 0, 0, 0);
+      } else {
+        o[(j - 16) & 3] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ring[j % 5], pb[(j - 16) >> 2], o[(j - 16) & 3], 0, 0, 0);
+      }
+    });
+    __builtin_amdgcn_s_setprio(0);
+  };
+  if (!group_b) {
+    // group A: phase 2t MFMA, phase 2t+1 softmax(t+1) + V(t+1) staging
+    auto step = [&](auto PAR, int t) __attribute__((always_inline)) {
+      constexpr int par = decltype(PAR)::value;
+      mfma_phase(PAR);
+      ATTN_STAMP(t, 0);
+      __syncthreads();
+      ATTN_STAMP(t, 1);
+      if (t + 1 < ntiles) {
+        softmax(t + 1);
+        write_v(std::integral_constant<int, par ^ 1>{});
+        load_tile(t + 2);
+      }
+      ATTN_STAMP(t, 2);
+      __syncthreads();
+      ATTN_STAMP(t, 3);
+    };
+    for (int t = 0; t < ntiles; t += 2) {
+      step(B0{}, t);
+      if (t + 1 >= ntiles) break;
+      step(B1{}, t + 1);
+    }
+  } else {
+    // group B: phase 2t softmax(t) + K(t+2) staging, phase 2t+1 MFMA
+    auto step = [&](auto PAR, int t) __attribute__((always_inline)) {
+      softmax(t);
+      if (t + 2 < ntiles) {
+        write_k(PAR);
+        load_tile(t + 3);
+      }
+      ATTN_STAMP(t, 0);
+      __syncthreads();
+      ATTN_STAMP(t, 1);
+      mfma_phase(PAR);
+      ATTN_STAMP(t, 2);
+      __syncthreads();
+      ATTN_STAMP(t, 3);
+    };
+    for (int t = 0; t < ntiles; t += 2) {
+      step(B0{}, t);
+      if (t + 1 >= ntiles) break;
+      step(B1{}, t + 1);
+    }
   }
 
   // ---- epilogue: O = O^T / l, bf16, row q, d = 32db + 8g + 4hl + (0..3) ----
@@ -283,6 +387,12 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
 
 }  // namespace
 
+#ifdef CP25_ATTN_PROBE
+static unsigned long long* g_probe = nullptr;
+static int g_probe_t0 = 0;
+extern "C" void cp25_attn_probe_set(unsigned long long* probe, int t0) { g_probe = probe; g_probe_t0 = t0; }
+#endif
+
 extern "C" int cp25_attn_fwd(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq,
                              int Lk, int D, const int64_t* q_strides, const int64_t* k_strides,
                              const int64_t* v_strides, const int64_t* o_strides, float softmax_scale,
@@ -295,6 +405,10 @@ extern "C" int cp25_attn_fwd(const void* q, const void* k, const void* v, void* 
   for (int i = 0; i < 4; ++i)
     for (int j = 0; j < 3; ++j)
       if (ss[i][j] % 8 != 0) return CP25_ERR_INVAL;
+  // buffer_load offsets within a 64-key tile are 32-bit
+  if ((int64_t)kKBlk * k_strides[1] * 2 >= (1ll << 31) || (int64_t)kKBlk * v_strides[1] * 2 >= (1ll << 31))
+    return CP25_ERR_INVAL;
+  if (k_strides[1] <= 0 || v_strides[1] <= 0) return CP25_ERR_INVAL;
   if (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) & 15) return CP25_ERR_INVAL;
   AttnArgs a;
   a.q = (const unsigned short*)q; a.k = (const unsigned short*)k; a.v = (const unsigned short*)v;
@@ -306,6 +420,10 @@ extern "C" int cp25_attn_fwd(const void* q, const void* k, const void* v, void* 
   a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk;
   a.nqb = (int)cdiv(Lq, kQBlk);
   a.scale_log2 = softmax_scale * 1.4426950408889634f;
+#ifdef CP25_ATTN_PROBE
+  a.probe = g_probe;
+  a.probe_t0 = g_probe_t0;
+#endif
   const int64_t nwg = (int64_t)a.nqb * B * H;
   if (nwg > 0x7fffffff) return CP25_ERR_INVAL;
   if (Lk <= 4096)

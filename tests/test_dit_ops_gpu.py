@@ -54,7 +54,7 @@ def test_ln_mod_with_residual(device):
 
 
 def test_ln_mod_broadcast_input(device):
-    n, B, D, T, hw = 64, 2, 512, 2, 32
+    n, B, D, T, hw = 64, 2, 512, 3, 32  # tokens 32..95 span frames 1..2
     g = torch.Generator().manual_seed(1)
     x = torch.randn(n, 1, D, generator=g).to(device, torch.bfloat16)
     mods = (torch.randn(B, T, 3 * D, generator=g) * 0.5).to(device, torch.bfloat16)

@@ -23,13 +23,28 @@ def main():
     ap.add_argument("--B", type=int, default=2)
     ap.add_argument("--H", type=int, default=16)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--fused", action="store_true",
+                    help="q/k/v as strided views of a token-major [L, B, 3*H*128] QKV buffer (the DiT's layout)")
+    ap.add_argument("--zeros", action="store_true", help="zero-filled inputs (DVFS reference point)")
+    ap.add_argument("--lib", default="", help="lab build of libcp25.so to load instead of the in-tree one")
     a = ap.parse_args()
+    if a.lib:
+        N._LIB_PATH = a.lib
     dev = torch.device("cuda:0")
     Lk = a.Lk or a.L
     g = torch.Generator(device=dev).manual_seed(0)
-    q = torch.randn(a.B, a.L, a.H, 128, device=dev, generator=g).to(torch.bfloat16)
-    k = torch.randn(a.B, Lk, a.H, 128, device=dev, generator=g).to(torch.bfloat16)
-    v = torch.randn(a.B, Lk, a.H, 128, device=dev, generator=g).to(torch.bfloat16)
+    if a.fused:
+        assert Lk == a.L
+        D = a.H * 128
+        buf = torch.randn(a.L, a.B, 3 * D, device=dev, generator=g).to(torch.bfloat16)
+        q, k, v = (buf[:, :, i * D:(i + 1) * D].view(a.L, a.B, a.H, 128).transpose(0, 1) for i in range(3))
+    else:
+        q = torch.randn(a.B, a.L, a.H, 128, device=dev, generator=g).to(torch.bfloat16)
+        k = torch.randn(a.B, Lk, a.H, 128, device=dev, generator=g).to(torch.bfloat16)
+        v = torch.randn(a.B, Lk, a.H, 128, device=dev, generator=g).to(torch.bfloat16)
+    if a.zeros:
+        for t in (q, k, v):
+            t.zero_()
     o = N.attn_fwd(q, k, v)
     torch.cuda.synchronize()
     st = torch.cuda.current_stream()
@@ -42,7 +57,8 @@ def main():
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
     flop = 4.0 * a.B * a.H * a.L * Lk * 128
-    print(json.dumps({"kernel": "attn_fwd", "B": a.B, "H": a.H, "Lq": a.L, "Lk": Lk, "ms": ms,
+    print(json.dumps({"kernel": "attn_fwd", "B": a.B, "H": a.H, "Lq": a.L, "Lk": Lk, "fused": a.fused,
+                      "zeros": a.zeros, "iters": a.iters, "lib": os.path.basename(a.lib) or "libcp25.so", "ms": ms,
                       "tflops": flop / ms / 1e9}))
 
 
