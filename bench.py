@@ -28,6 +28,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "frames/sec, Predict2.5-2B Image2World 720p×121f, 35 UniPC steps, CP=1/8"
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 MFMA
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1", "attn_pmc_r1c", "SUMMARY.json")
 
 
 def parse():
@@ -112,6 +113,14 @@ def main():
     if rank == 0:
         ms = elapsed / a.steps * 1e3
         valid = a.num_steps == 35 and a.frames == 121 and (h, w) == (704, 1280)
+        # HBM bytes per self-attention launch from the committed rocprofv3 PMC passes of this kernel
+        # at this shape (tools/pmc_attn.sh, FETCH_SIZE x2 gfx950 correction + WRITE_SIZE); only the
+        # CP = 1 metric shape was measured, so other shapes report null
+        traffic, traffic_src = None, None
+        if world == 1 and valid and os.path.exists(PMC_SUMMARY):
+            with open(PMC_SUMMARY) as f:
+                traffic = json.load(f).get("traffic_bytes_per_launch")
+            traffic_src = os.path.relpath(PMC_SUMMARY, ROOT)
         line = {
             "metric": METRIC,
             "value": frames * a.steps / elapsed,
@@ -141,7 +150,8 @@ def main():
                 "peak": BF16_DENSE_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved / BF16_DENSE_PEAK_TFLOPS,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "launches_timed": len(attn_ms),
                 "avg_launch_ms": attn_avg_s * 1e3,
                 "flop_per_launch": attn_flop,
