@@ -49,6 +49,10 @@ _F = ctypes.c_float
 # symbol -> argtypes (restype is always int)
 SIGNATURES = {
     "cp25_attn_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, c_int64_p, _F, _P],
+    "cp25_attn_fwd_split": [_P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, c_int64_p, _F, _I,
+                            _P, ctypes.c_size_t, _P],
+    "cp25_attn_workspace_bytes": [_I, _I, _I, _I],
+    "cp25_attn_plan": [_I, _I, _I, _I, _I],
     "cp25_ln_mod": [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _P, _P, _I64, _I, _I, _I64, _I64, _F, _P],
     "cp25_final_ln_mod": [_P, _P, _P, _I64, _I64, _P, _P, _I64, _I64, _P, _I64, _I, _I, _I64, _I64, _F, _P],
     "cp25_head_rmsnorm_rope": [_P, _I64, _I64, _I, _I, _I, _P, _P, _P, _P, _I64, _F, _P],
@@ -86,7 +90,7 @@ def load_library() -> ctypes.CDLL:
             raise RuntimeError(f"libcp25.so does not export {name}")
         if argtypes is not None:
             fn.argtypes = argtypes
-        fn.restype = ctypes.c_int
+        fn.restype = ctypes.c_size_t if name == "cp25_attn_workspace_bytes" else ctypes.c_int
     _lib = lib
     return lib
 
@@ -120,10 +124,18 @@ def _i64x3(vals) -> ctypes.Array:
 
 
 # ----------------------------------------------------------------------------- attention
+def attn_plan(B: int, H: int, Lq: int, Lk: int, D: int = 128) -> int:
+    """Key-range split the library picks for this shape (cp25_attn_plan)."""
+    n = load_library().cp25_attn_plan(B, H, Lq, Lk, D)
+    _check("cp25_attn_plan", min(n, 0))
+    return n
+
+
 def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[torch.Tensor] = None,
-             softmax_scale: Optional[float] = None) -> torch.Tensor:
+             softmax_scale: Optional[float] = None, n_split: Optional[int] = None) -> torch.Tensor:
     """softmax(q k^T * scale) v for q [B, Lq, H, 128], k/v [B, Lk, H, 128] (bf16, any strides with
-    a contiguous head dim). Returns [B, Lq, H, 128] bf16."""
+    a contiguous head dim). Returns [B, Lq, H, 128] bf16. n_split: key-range split (None = the
+    library's plan for this shape; the fp32 partials live in a caching-allocator workspace)."""
     lib = load_library()
     if q.dtype != torch.bfloat16 or k.dtype != torch.bfloat16 or v.dtype != torch.bfloat16:
         raise ValueError("attn_fwd expects bf16 q/k/v (attention() recasts to bf16 first)")
@@ -137,15 +149,20 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
     if out is None:
         out = torch.empty((B, Lq, H, D), dtype=torch.bfloat16, device=q.device)
     scale = float(D) ** -0.5 if softmax_scale is None else float(softmax_scale)
-    rc = lib.cp25_attn_fwd(
+    if n_split is None:
+        forced = os.environ.get("CP25_ATTN_SPLIT")  # e.g. "1": never split (bitwise CP=N vs CP=1 checks)
+        n_split = min(int(forced), (Lk + 63) // 64) if forced else attn_plan(B, H, Lq, Lk, D)
+    ws_bytes = lib.cp25_attn_workspace_bytes(B, H, Lq, n_split)
+    ws = torch.empty(((ws_bytes + 15) // 16 * 4,), dtype=torch.float32, device=q.device) if ws_bytes else None
+    rc = lib.cp25_attn_fwd_split(
         _ptr(q), _ptr(k), _ptr(v), _ptr(out), B, H, Lq, Lk, D,
         _i64x3((q.stride(0), q.stride(1), q.stride(2))),
         _i64x3((k.stride(0), k.stride(1), k.stride(2))),
         _i64x3((v.stride(0), v.stride(1), v.stride(2))),
         _i64x3((out.stride(0), out.stride(1), out.stride(2))),
-        scale, _stream(q.device),
+        scale, int(n_split), _ptr(ws), ws_bytes, _stream(q.device),
     )
-    _check("cp25_attn_fwd", rc)
+    _check("cp25_attn_fwd_split", rc)
     return out
 
 

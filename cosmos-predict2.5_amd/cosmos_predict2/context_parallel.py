@@ -50,6 +50,31 @@ def all_gather_into(out: torch.Tensor, x: torch.Tensor, group) -> torch.Tensor:
     return out
 
 
+class _Done:
+    """Handle of a collective that already completed (gloo staging path)."""
+
+    def wait(self) -> bool:
+        return True
+
+
+def all_gather_into_async(out: torch.Tensor, x: torch.Tensor, group):
+    """Asynchronous all_gather_into: returns a handle whose .wait() makes the CURRENT stream wait for
+    the gather. With RCCL the gather runs on the process group's own stream, ordered after the work
+    already queued on the current stream (so x is complete), and overlaps whatever the current
+    stream does next; the gloo path (tests) completes before returning."""
+    if dist.get_backend(group) == "gloo" and x.is_cuda:
+        all_gather_into(out, x, group)
+        return _Done()
+    return dist.all_gather_into_tensor(out, x.contiguous(), group=group, async_op=True)
+
+
+def kv_chunk_views(kv_all_c: torch.Tensor, n_tok_total: int, B: int, Hc: int, hd: int):
+    """K and V [B, L, Hc, hd] views of one gathered head chunk [L*B, 2*Hc*hd] (rows token-major,
+    batch inner; each row = Hc K heads then Hc V heads), as the attention kernel reads them."""
+    kc = kv_all_c.view(n_tok_total, B, 2, Hc, hd)
+    return kc[:, :, 0].transpose(0, 1), kc[:, :, 1].transpose(0, 1)
+
+
 def gather_tokens(x: torch.Tensor, group) -> torch.Tensor:
     """Concatenate every rank's token shard along dim 0 (cat_outputs_cp on the token axis)."""
     r, w = cp_rank_world(group)

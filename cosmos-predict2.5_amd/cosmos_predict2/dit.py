@@ -23,7 +23,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _native as N
-from .context_parallel import all_gather_into
+from .context_parallel import all_gather_into_async, kv_chunk_views
 from .net_config import DiTConfig
 
 BF16 = torch.bfloat16
@@ -166,6 +166,8 @@ class MinimalV1LVGDiT:
         self.sd: Dict[str, torch.Tensor] = {}
         self._rope_cache: Dict[Tuple[int, int, int], Tuple[torch.Tensor, torch.Tensor]] = {}
         self.cp_group = None
+        self._lane_streams: List[torch.cuda.Stream] = []  # CP > 1: one stream per CFG batch entry
+        self.force_lanes = False  # run the per-batch-entry lanes at CP = 1 too (CP parity tests)
         # optional list collecting (start, end, flop) HIP events around every self-attention launch
         self.attn_events: Optional[list] = None
 
@@ -284,11 +286,16 @@ class MinimalV1LVGDiT:
                        geo: Geometry) -> torch.Tensor:
         """patch_rows: [n_tok, Bx, 72] bf16 (Bx = 1 shares the input across the CFG batch);
         t_B_T: [B, T] fp32, already scaled. Returns the final layer output [n_tok, B, 64] fp32
-        (feature order (p1 p2 C) = patch layout)."""
+        (feature order (p1 p2 C) = patch layout).
+
+        CP = 1: one pass over the batch (B = 2 = [cond, uncond]) on the current stream.
+        CP > 1: the batch entries run as two lanes on their own streams, issued block by block in
+        alternation; each lane's self-attention waits for its own K/V all-gather, so one lane's
+        RCCL transfer overlaps the other lane's compute (lane 1 starts half a block behind)."""
         cfg = self.cfg
         p = self.sd
         B = ctx.B
-        D, H, hd = cfg.model_channels, cfg.num_heads, cfg.head_dim
+        D = cfg.model_channels
         n = geo.n_tok
         Bx = patch_rows.shape[1]
         x_in = F.linear(patch_rows.reshape(n * Bx, -1), p["x_embedder.proj.1.weight"]).view(n, Bx, D)
@@ -296,6 +303,63 @@ class MinimalV1LVGDiT:
         cos, sin = self.rope_tables(geo)
         cp = self.cp_group
         cp_size = 1 if cp is None else torch.distributed.get_world_size(cp)
+        if B == 1 or (cp_size == 1 and not self.force_lanes):
+            gen = self._blocks(x_in, mods, shift_f, scale_f, ctx, geo, cos, sin, cp, cp_size)
+            while True:
+                try:
+                    next(gen)
+                except StopIteration as e:
+                    return e.value
+        cur = torch.cuda.current_stream(self.device)
+        if len(self._lane_streams) < B:
+            self._lane_streams = [torch.cuda.Stream(device=self.device) for _ in range(B)]
+        ready = torch.cuda.Event()
+        ready.record(cur)
+        phase = torch.cuda.Event()
+        lanes = []
+        for b in range(B):
+            st = self._lane_streams[b]
+            st.wait_event(ready)
+            cb = ContextCache(B=1, k=[t[b:b + 1] for t in ctx.k], v=[t[b:b + 1] for t in ctx.v])
+            xb = x_in[:, (0 if Bx == 1 else b):(0 if Bx == 1 else b) + 1]
+            with torch.cuda.stream(st):
+                gen = self._blocks(xb, mods[:, :, b:b + 1], shift_f[b:b + 1], scale_f[b:b + 1], cb, geo, cos, sin,
+                                   cp, cp_size, phase_event=phase if b == 0 else None)
+            lanes.append([st, gen, None])
+        live = B
+        first = True
+        while live:
+            for b, lane in enumerate(lanes):
+                if lane[1] is None:
+                    continue
+                if first and b == 1:
+                    lane[0].wait_event(phase)  # lane 0 recorded it once its first K/V gather was queued
+                with torch.cuda.stream(lane[0]):
+                    try:
+                        next(lane[1])
+                    except StopIteration as e:
+                        lane[2] = e.value
+                        lane[1] = None
+                        live -= 1
+            first = False
+        for st, _, o in lanes:
+            cur.wait_stream(st)
+            o.record_stream(cur)
+        for t in (x_in, mods, shift_f, scale_f, cos, sin):
+            for st, _, _ in lanes:
+                t.record_stream(st)
+        return torch.cat([o for _, _, o in lanes], dim=1)
+
+    def _blocks(self, x_in, mods, shift_f, scale_f, ctx: ContextCache, geo: Geometry, cos, sin, cp, cp_size,
+                phase_event=None):
+        """Generator: issues the 28 blocks + final layer for the batch entries in x_in/mods/ctx on the
+        current stream, yielding after each block; returns the final layer output [n, B, 64] fp32."""
+        cfg = self.cfg
+        p = self.sd
+        B = ctx.B
+        D, H, hd = cfg.model_channels, cfg.num_heads, cfg.head_dim
+        n = geo.n_tok
+        Bx = x_in.shape[1]
 
         def mod(i, j):  # (shift, scale, gate) bf16 [B, T, D] views of block i, sub-layer j
             m = mods[i, j]
@@ -304,48 +368,47 @@ class MinimalV1LVGDiT:
         common = dict(n_tok=n, B=B, tok0=geo.tok0, hw=geo.hw)
         sh, sc, _ = mod(0, 0)
         x = x_in
-        h = N.ln_mod(x, sh, sc, x_st=Bx * D, x_sb=0 if Bx == 1 else D, **common)
+        h = N.ln_mod(x, sh, sc, x_st=x_in.stride(0), x_sb=0 if Bx == 1 else x_in.stride(1), **common)
         y = None
         gate_prev = None
         scale_attn = hd ** -0.5
         for i in range(cfg.num_blocks):
             pre = f"blocks.{i}."
             # ---- self attention
-            qkv = F.linear(h.view(n * B, D), self.w_qkv[i])  # [n*B, 3D]
-            N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=0, weight=p[pre + "self_attn.q_norm.weight"],
-                                cos=cos, sin=sin)
-            q = qkv.view(n, B, 3 * D)[:, :, :D].view(n, B, H, hd).transpose(0, 1)
+            o = torch.empty((n, B, D), dtype=BF16, device=self.device)
+            ev = None
+            if self.attn_events is not None:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             if cp is None or cp_size == 1:
+                qkv = F.linear(h.view(n * B, D), self.w_qkv[i])  # [n*B, 3D]
+                N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=0,
+                                    weight=p[pre + "self_attn.q_norm.weight"], cos=cos, sin=sin)
                 N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=D,
                                     weight=p[pre + "self_attn.k_norm.weight"], cos=cos, sin=sin)
+                q = qkv.view(n, B, 3 * D)[:, :, :D].view(n, B, H, hd).transpose(0, 1)
                 kk = qkv.view(n, B, 3 * D)[:, :, D:2 * D].view(n, B, H, hd).transpose(0, 1)
                 vv = qkv.view(n, B, 3 * D)[:, :, 2 * D:].view(n, B, H, hd).transpose(0, 1)
+                if ev is not None:
+                    ev[0].record()
+                N.attn_fwd(q, kk, vv, out=o.view(n, B, H, hd).transpose(0, 1), softmax_scale=scale_attn)
+                lk = kk.shape[1]
             else:
-                kv_loc = torch.empty((n, B, 2 * D), dtype=BF16, device=self.device)
-                N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=D,
-                                    weight=p[pre + "self_attn.k_norm.weight"], cos=cos, sin=sin,
-                                    out2=kv_loc, out2_stride=2 * D)
-                N.copy_rows(qkv, 3 * D, kv_loc.view(n * B, 2 * D)[:, D:], 2 * D, n * B, D, src_offset=2 * D)
-                kv = torch.empty((cp_size * n, B, 2 * D), dtype=BF16, device=self.device)
-                all_gather_into(kv, kv_loc, cp)  # RCCL over xGMI
-                kk = kv[:, :, :D].view(cp_size * n, B, H, hd).transpose(0, 1)
-                vv = kv[:, :, D:].view(cp_size * n, B, H, hd).transpose(0, 1)
-            o = torch.empty((n, B, D), dtype=BF16, device=self.device)
-            if self.attn_events is not None:
-                e0 = torch.cuda.Event(enable_timing=True)
-                e1 = torch.cuda.Event(enable_timing=True)
-                e0.record()
-            N.attn_fwd(q, kk, vv, out=o.view(n, B, H, hd).transpose(0, 1), softmax_scale=scale_attn)
-            if self.attn_events is not None:
-                e1.record()
-                self.attn_events.append((e0, e1, 4.0 * B * H * n * kk.shape[1] * hd))
+                self._cp_self_attention(i, h, o, cos, sin, n, B, cp, cp_size, ev[0] if ev is not None else None,
+                                        phase_event if i == 0 else None)
+                lk = cp_size * n
+            if ev is not None:
+                ev[1].record()
+                self.attn_events.append((ev[0], ev[1], 4.0 * B * H * n * lk * hd))
             y = F.linear(o.view(n * B, D), p[pre + "self_attn.output_proj.weight"])
             # ---- x += g_sa * y ; LN-mod for cross attention
             _, _, g_sa = mod(i, 0)
             sh, sc, _ = mod(i, 1)
             x_new = torch.empty((n, B, D), dtype=BF16, device=self.device)
-            h = N.ln_mod(x, sh, sc, x_st=(Bx if i == 0 else B) * D, x_sb=(0 if (i == 0 and Bx == 1) else D),
-                         y=y, gate=g_sa, x_out=x_new, **common)
+            if i == 0:
+                x_st, x_sb = x_in.stride(0), (0 if Bx == 1 else x_in.stride(1))
+            else:
+                x_st, x_sb = B * D, D
+            h = N.ln_mod(x, sh, sc, x_st=x_st, x_sb=x_sb, y=y, gate=g_sa, x_out=x_new, **common)
             x = x_new
             # ---- cross attention
             qc = F.linear(h.view(n * B, D), p[pre + "cross_attn.q_proj.weight"])
@@ -370,10 +433,40 @@ class MinimalV1LVGDiT:
                 x_new = torch.empty((n, B, D), dtype=BF16, device=self.device)
                 h = N.ln_mod(x, sh, sc, x_st=B * D, x_sb=D, y=y, gate=gate_prev, x_out=x_new, **common)
                 x = x_new
+            yield i
         # ---- final layer (fp32 autocast): x + g*y -> LN -> modulate -> Linear(D -> 64)
         xf = N.final_ln_mod(x, shift_f, scale_f, y=y, gate=gate_prev, **common)
         out = F.linear(xf.view(n * B, D), self.w_final)
         return out.view(n, B, -1)
+
+    def _cp_self_attention(self, i: int, h: torch.Tensor, o: torch.Tensor, cos, sin, n: int, B: int, cp,
+                           cp_size: int, e0=None, phase_event=None) -> None:
+        """Self-attention of a context-parallel token shard (replaces the reference's Ulysses
+        all-to-all, a2a_cp.py:160-219, which needs T % cp == 0): the shard's normed + roped K|V rows
+        are all-gathered from every rank over RCCL, asynchronously (the other lane computes
+        meanwhile); the attention waits for the gather only. The launch is unsplit: the two lanes'
+        kernels run concurrently and fill each other's tails. Same QKV GEMM and norm as CP = 1."""
+        cfg = self.cfg
+        p = self.sd
+        pre = f"blocks.{i}."
+        D, H, hd = cfg.model_channels, cfg.num_heads, cfg.head_dim
+        qkv = F.linear(h.view(n * B, D), self.w_qkv[i])  # [n*B, 3D]
+        N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=D, weight=p[pre + "self_attn.k_norm.weight"],
+                            cos=cos, sin=sin)
+        kv = torch.empty((n * B, 2 * D), dtype=BF16, device=self.device)
+        N.copy_rows(qkv, 3 * D, kv, 2 * D, n * B, 2 * D, src_offset=D)
+        kv_all = torch.empty((cp_size * n * B, 2 * D), dtype=BF16, device=self.device)
+        work = all_gather_into_async(kv_all, kv, cp)  # RCCL over xGMI
+        if phase_event is not None:
+            phase_event.record()
+        N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=0, weight=p[pre + "self_attn.q_norm.weight"],
+                            cos=cos, sin=sin)
+        work.wait()
+        if e0 is not None:
+            e0.record()
+        kc, vc = kv_chunk_views(kv_all, cp_size * n, B, H, hd)
+        q = qkv.view(n, B, 3 * D)[:, :, :D].view(n, B, H, hd).transpose(0, 1)
+        N.attn_fwd(q, kc, vc, out=o.view(n, B, H, hd).transpose(0, 1), softmax_scale=hd ** -0.5, n_split=1)
 
     # ---------------------------------------------------------------- reference-compatible forward
     @torch.no_grad()

@@ -79,6 +79,10 @@ struct AttnArgs {
   int64_t o_sb, o_sl, o_sh;
   int B, H, Lq, Lk;
   int nqb;          // query blocks per (b, h)
+  int nsplit;       // key-range splits per (b, h, query block) (1: O written directly)
+  int tps;          // key tiles per split
+  float* o_part;    // nsplit > 1: [nsplit][B][H][Lq][128] fp32 partial O (normalised per split)
+  float* lse_part;  // nsplit > 1: [nsplit][B][H][Lq] fp32 log2-sum-exp2 of the scaled scores
   float scale_log2; // softmax scale * log2(e)
 #ifdef CP25_ATTN_PROBE
   unsigned long long* probe;  // [wg < 8][wave][tile - probe_t0 < 32][4] s_memtime stamps (lab build only)
@@ -117,8 +121,13 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
 
   const int nwg = gridDim.x;
   const int tile = xcd_remap(blockIdx.x, nwg);
-  const int bh = tile / a.nqb, qb = tile % a.nqb;
+  // tile order (b, h) > split > query block: an XCD's contiguous tile range streams one key range
+  const int qb = tile % a.nqb, bhs = tile / a.nqb;
+  const int split = bhs % a.nsplit, bh = bhs / a.nsplit;
   const int b = bh / a.H, h = bh % a.H;
+  // this workgroup's keys: [split * tps * 64, ...) as a self-contained key sequence of length Lk
+  const int key0 = split * a.tps * kKBlk;
+  const int Lk = min(a.Lk - key0, a.tps * kKBlk);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -128,8 +137,8 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   const bool group_b = __builtin_amdgcn_readfirstlane(tid) >= kThreads / 2;
 
   const unsigned short* qp = a.q + b * a.q_sb + h * a.q_sh;
-  const unsigned short* kp = a.k + b * a.k_sb + h * a.k_sh;
-  const unsigned short* vp = a.v + b * a.v_sb + h * a.v_sh;
+  const unsigned short* kp = a.k + b * a.k_sb + h * a.k_sh + (int64_t)key0 * a.k_sl;
+  const unsigned short* vp = a.v + b * a.v_sb + h * a.v_sh + (int64_t)key0 * a.v_sl;
 
   // ---- Q fragments (B operand of S^T = K Q^T): Q[q][16s + 8hl .. +7], s = 0..7 ----
   const int q_row = qb * kQBlk + wave * kQRows + l31;
@@ -149,7 +158,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   float m_run = -1e30f;
   float l_run = 0.f;
 
-  const int ntiles = (a.Lk + kKBlk - 1) / kKBlk;
+  const int ntiles = (Lk + kKBlk - 1) / kKBlk;
 
   // staging: a group's 256 threads own 4 chunks (16 B) each of a 64x128 tile: rows u/16 + 16 i,
   // chunk u%16. buffer_load: the tile base is a wave-uniform descriptor (SALU only), the per-lane
@@ -162,7 +171,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   const int st_off = (int)(srow * sl * 2) + sch * 16, st_step = (int)(16 * sl * 2);
   u32x4 st[4];
   auto load_tile = [&](int t) __attribute__((always_inline)) {
-    const int rows = min(a.Lk - t * kKBlk, kKBlk);
+    const int rows = min(Lk - t * kKBlk, kKBlk);
     const int nbytes = rows > 0 ? (int)((rows - 1) * sl * 2) + 2 * kD : 0;
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(sbase + (int64_t)t * kKBlk * sl), (short)0, nbytes,
                                                         0x00020000);
@@ -193,7 +202,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   const unsigned v_rd_lds = (unsigned)(uintptr_t)(lds_char_ptr)v_rd;
 
   // ragged last tile: keys >= Lk get a -inf score (a uniform branch taken on that tile only)
-  const int ragged_tile = (a.Lk % kKBlk) != 0 ? a.Lk / kKBlk : -1;
+  const int ragged_tile = (Lk % kKBlk) != 0 ? Lk / kKBlk : -1;
 
   f32x16 S[2];   // S^T of the tile awaiting its softmax
   bf16x8 pb[4];  // P^T of the tile awaiting its P.V
@@ -219,7 +228,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int key = t * kKBlk + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-          if (key >= a.Lk) S[kt][r] = -INFINITY;
+          if (key >= Lk) S[kt][r] = -INFINITY;
         }
     }
     // four independent v_max3 chains (this file builds with -fno-honor-nans: no canonicalising
@@ -371,6 +380,25 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   // ---- epilogue: O = O^T / l, bf16, row q, d = 32db + 8g + 4hl + (0..3) ----
   const float l_tot = wave_swap_sum(l_run);
   const float inv = 1.f / l_tot;
+  if (a.nsplit > 1) {
+    // partial O of this key range (fp32, normalised by its own sum) + its log2-sum-exp2; merged by
+    // attn_merge_splits
+    if (q_row < a.Lq) {
+      const int64_t row = ((int64_t)(split * a.B + b) * a.H + h) * a.Lq + q_row;
+      float* op = a.o_part + row * kD;
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          f32x4 w;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[e] = o[db][4 * g + e] * inv;
+          *reinterpret_cast<f32x4*>(op + 32 * db + 8 * g + 4 * hl) = w;
+        }
+      if (hl == 0) a.lse_part[row] = m_run + __log2f(l_tot);
+    }
+    return;
+  }
   if (q_row < a.Lq) {
     unsigned short* op = a.o + b * a.o_sb + h * a.o_sh + (int64_t)q_row * a.o_sl;
 #pragma unroll
@@ -385,6 +413,74 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   }
 }
 
+// O[b, q, h, :] = sum_s w_s O_s / sum_s w_s with w_s = exp2(lse_s - max_s lse_s): the key-range
+// partials of one (b, h, q) row combined exactly as the online softmax would have. One thread per
+// 4 head-dim elements (32 threads per row); HBM-bound.
+__global__ void __launch_bounds__(256) attn_merge_splits(const float* __restrict__ o_part,
+                                                        const float* __restrict__ lse_part, unsigned short* o,
+                                                        int nsplit, int B, int H, int Lq, int64_t o_sb,
+                                                        int64_t o_sl, int64_t o_sh) {
+  const int64_t rows = (int64_t)B * H * Lq;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t row = gid >> 5;
+  if (row >= rows) return;
+  const int d = (int)(gid & 31) * 4;
+  float mx = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) mx = fmaxf(mx, lse_part[s * rows + row]);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float den = 0.f;
+  for (int s = 0; s < nsplit; ++s) {
+    const float w = __builtin_amdgcn_exp2f(lse_part[s * rows + row] - mx);
+    const f32x4 v = *reinterpret_cast<const f32x4*>(o_part + (s * rows + row) * kD + d);
+    acc += w * v;
+    den += w;
+  }
+  const float inv = 1.f / den;
+  const int q = (int)(row % Lq);
+  const int bh = (int)(row / Lq);
+  const int b = bh / H, h = bh % H;
+  u16x4 w;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) w[e] = f2bf(acc[e] * inv);
+  *reinterpret_cast<u16x4*>(o + b * o_sb + (int64_t)q * o_sl + h * o_sh + d) = w;
+}
+
+int g_num_cus = 0;
+
+int num_cus() {
+  if (g_num_cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    g_num_cus = n;
+  }
+  return g_num_cus;
+}
+
+// Work-balance model for the key-range split: the kernel holds one workgroup per CU (252 VGPRs,
+// 2 waves/SIMD), every workgroup's time is ~ its key tiles + a fixed ~44 tiles, and workgroups run
+// in ceil(nwg / CUs) rounds; a split adds the fp32 partial write + merge traffic (~1 tile of time per
+// 9 MB at HBM rate). The fixed cost is fitted to MI355X measurements (tools/bench_cp_chunks.py:
+// B 2, H 16, Lq 13640, Lk 109120 ran 21.9 ms unsplit vs 23.0 ms at split 4; H 4: 6.24 vs 6.14 ms):
+// shorter workgroups lose the lock-step K/V streaming through the XCD's L2 that long ones keep.
+// Picks the split with the least modelled time.
+int plan_split(int B, int H, int Lq, int Lk) {
+  const int64_t nqb = cdiv(Lq, kQBlk), ntiles = cdiv(Lk, kKBlk);
+  const int64_t nwg = nqb * B * H, cus = num_cus();
+  int best = 1;
+  double best_cost = 1e300;
+  for (int s = 1; s <= 8 && s <= ntiles; ++s) {
+    const int64_t tps = cdiv(ntiles, s);
+    if (cdiv(ntiles, tps) != s) continue;  // every split must own at least one tile
+    const double rounds = (double)cdiv(nwg * s, cus);
+    double cost = rounds * (double)(tps + 44);
+    if (s > 1) cost += (2.0 * s + 0.5) * (double)B * H * Lq * kD * 4 / 9.0e6;
+    if (cost < best_cost * 0.995) { best_cost = cost; best = s; }
+  }
+  return best;
+}
+
 }  // namespace
 
 #ifdef CP25_ATTN_PROBE
@@ -393,10 +489,10 @@ static int g_probe_t0 = 0;
 extern "C" void cp25_attn_probe_set(unsigned long long* probe, int t0) { g_probe = probe; g_probe_t0 = t0; }
 #endif
 
-extern "C" int cp25_attn_fwd(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq,
-                             int Lk, int D, const int64_t* q_strides, const int64_t* k_strides,
-                             const int64_t* v_strides, const int64_t* o_strides, float softmax_scale,
-                             hipStream_t stream) {
+static int attn_launch(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq, int Lk, int D,
+                       const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
+                       const int64_t* o_strides, float softmax_scale, int n_split, void* workspace, size_t ws_bytes,
+                       hipStream_t stream) {
   if (D != kD) return CP25_ERR_DTYPE;
   if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0) return CP25_ERR_INVAL;
   if (!q || !k || !v || !o) return CP25_ERR_INVAL;
@@ -410,6 +506,15 @@ extern "C" int cp25_attn_fwd(const void* q, const void* k, const void* v, void* 
     return CP25_ERR_INVAL;
   if (k_strides[1] <= 0 || v_strides[1] <= 0) return CP25_ERR_INVAL;
   if (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) & 15) return CP25_ERR_INVAL;
+  const int64_t ntiles = cdiv(Lk, kKBlk);
+  if (n_split < 1 || n_split > ntiles) return CP25_ERR_INVAL;
+  const int64_t tps = cdiv(ntiles, n_split);
+  if (cdiv(ntiles, tps) != n_split) return CP25_ERR_INVAL;  // a split without keys
+  const int64_t rows = (int64_t)B * H * Lq;
+  if (n_split > 1) {
+    if (!workspace || ((uintptr_t)workspace & 15) || ws_bytes < cp25_attn_workspace_bytes(B, H, Lq, n_split))
+      return CP25_ERR_INVAL;
+  }
   AttnArgs a;
   a.q = (const unsigned short*)q; a.k = (const unsigned short*)k; a.v = (const unsigned short*)v;
   a.o = (unsigned short*)o;
@@ -419,17 +524,54 @@ extern "C" int cp25_attn_fwd(const void* q, const void* k, const void* v, void* 
   a.o_sb = o_strides[0]; a.o_sl = o_strides[1]; a.o_sh = o_strides[2];
   a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk;
   a.nqb = (int)cdiv(Lq, kQBlk);
+  a.nsplit = n_split;
+  a.tps = (int)tps;
+  a.o_part = n_split > 1 ? (float*)workspace : nullptr;
+  a.lse_part = n_split > 1 ? (float*)workspace + (size_t)n_split * rows * kD : nullptr;
   a.scale_log2 = softmax_scale * 1.4426950408889634f;
 #ifdef CP25_ATTN_PROBE
   a.probe = g_probe;
   a.probe_t0 = g_probe_t0;
 #endif
-  const int64_t nwg = (int64_t)a.nqb * B * H;
+  const int64_t nwg = (int64_t)a.nqb * B * H * n_split;
   if (nwg > 0x7fffffff) return CP25_ERR_INVAL;
   if (Lk <= 4096)
     hipLaunchKernelGGL(attn_fwd_d128<1>, dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
   else
     hipLaunchKernelGGL(attn_fwd_d128<0>, dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
   CP25_LAUNCH_CHECK();
+  if (n_split > 1) {
+    const int64_t threads = rows * 32;
+    hipLaunchKernelGGL(attn_merge_splits, dim3((unsigned)cdiv(threads, 256)), dim3(256), 0, stream, a.o_part,
+                       a.lse_part, a.o, n_split, B, H, Lq, a.o_sb, a.o_sl, a.o_sh);
+    CP25_LAUNCH_CHECK();
+  }
   return CP25_OK;
+}
+
+extern "C" size_t cp25_attn_workspace_bytes(int B, int H, int Lq, int n_split) {
+  if (n_split <= 1 || B <= 0 || H <= 0 || Lq <= 0) return 0;
+  return (size_t)n_split * B * H * Lq * (kD + 1) * sizeof(float);
+}
+
+extern "C" int cp25_attn_plan(int B, int H, int Lq, int Lk, int D) {
+  if (D != kD) return CP25_ERR_DTYPE;
+  if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0) return CP25_ERR_INVAL;
+  return plan_split(B, H, Lq, Lk);
+}
+
+extern "C" int cp25_attn_fwd(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq,
+                             int Lk, int D, const int64_t* q_strides, const int64_t* k_strides,
+                             const int64_t* v_strides, const int64_t* o_strides, float softmax_scale,
+                             hipStream_t stream) {
+  return attn_launch(q, k, v, o, B, H, Lq, Lk, D, q_strides, k_strides, v_strides, o_strides, softmax_scale, 1,
+                     nullptr, 0, stream);
+}
+
+extern "C" int cp25_attn_fwd_split(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq,
+                                   int Lk, int D, const int64_t* q_strides, const int64_t* k_strides,
+                                   const int64_t* v_strides, const int64_t* o_strides, float softmax_scale,
+                                   int n_split, void* workspace, size_t ws_bytes, hipStream_t stream) {
+  return attn_launch(q, k, v, o, B, H, Lq, Lk, D, q_strides, k_strides, v_strides, o_strides, softmax_scale,
+                     n_split, workspace, ws_bytes, stream);
 }

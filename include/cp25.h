@@ -35,6 +35,27 @@ int cp25_attn_fwd(const void* q, const void* k, const void* v, void* o, int B, i
                   const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
                   const int64_t* o_strides, float softmax_scale, hipStream_t stream);
 
+/* Key-range split ("split-KV") form of cp25_attn_fwd, same arguments and result: each (b, h, 256-query
+ * block) is processed by n_split workgroups over consecutive key ranges of ceil(ceil(Lk/64)/n_split)
+ * 64-key tiles, which write fp32 partial outputs + log-sum-exp into `workspace`
+ * (>= cp25_attn_workspace_bytes(B, H, Lq, n_split) bytes, 16-B aligned), merged into o by a second,
+ * stream-ordered launch. Used where B*H*ceil(Lq/256) workgroups would leave the last round of CUs
+ * mostly idle (a context-parallel shard's queries against the gathered keys, a head chunk of the
+ * K/V all-gather pipeline). n_split = 1 is cp25_attn_fwd. Same reference interface as cp25_attn_fwd;
+ * the split is the MI355X work decomposition, the result equals the unsplit softmax up to fp32/bf16
+ * rounding. */
+int cp25_attn_fwd_split(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq, int Lk, int D,
+                        const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
+                        const int64_t* o_strides, float softmax_scale, int n_split, void* workspace,
+                        size_t ws_bytes, hipStream_t stream);
+
+/* Bytes of workspace cp25_attn_fwd_split needs (0 for n_split <= 1). */
+size_t cp25_attn_workspace_bytes(int B, int H, int Lq, int n_split);
+
+/* The key-range split the library picks for this shape on the current device (>= 1; a round model of
+ * one workgroup per CU), or a negative error code. */
+int cp25_attn_plan(int B, int H, int Lq, int Lk, int D);
+
 /* ---------------------------------------------------------------- DiT block elementwise
  * Activations are token-major [n_tok, B, D] bf16 (batch inner). Row (tok, b) uses modulation row
  * (b, t) with t = (tok0 + tok) / hw (frame index; tok0 = first global token of this CP shard).

@@ -94,3 +94,42 @@ def test_attn_rejects_bad_args(device):
     q = torch.zeros(1, 8, 1, 64, dtype=torch.bfloat16, device=device)
     with pytest.raises(ValueError):
         N.attn_fwd(q, q, q)
+
+
+@pytest.mark.parametrize("B,H,Lq,Lk,n_split", [(1, 2, 300, 1030, 2), (2, 3, 513, 640, 3), (1, 1, 64, 130, 3),
+                                               (2, 2, 256, 4160, 8), (1, 4, 700, 64, 1)])
+def test_attn_split_matches_fp32(device, B, H, Lq, Lk, n_split):
+    """Key-range split (cp25_attn_fwd_split): fp32 partials + log-sum-exp merge; ragged last range."""
+    g = torch.Generator(device="cpu").manual_seed(99 + Lq + n_split)
+    q = torch.randn(B, Lq, H, 128, generator=g).to(device, torch.bfloat16)
+    k = torch.randn(B, Lk, H, 128, generator=g).to(device, torch.bfloat16)
+    v = torch.randn(B, Lk, H, 128, generator=g).to(device, torch.bfloat16)
+    o = N.attn_fwd(q, k, v, n_split=n_split)
+    ref = ref_attention(q, k, v)
+    assert rel_l2(o, ref) <= TOL, rel_l2(o, ref)
+    o1 = N.attn_fwd(q, k, v, n_split=1)
+    # split and unsplit differ only by P rounding against different running maxima
+    assert rel_l2(o, o1) <= TOL
+
+
+def test_attn_split_spike_in_one_range(device):
+    """A key that dominates one query's softmax lives in the last split only: the merge weights
+    (exp2 of the per-range log-sum-exp) must carry it."""
+    B, H, Lq, Lk = 1, 1, 256, 1024
+    g = torch.Generator(device="cpu").manual_seed(5)
+    q = torch.randn(B, Lq, H, 128, generator=g)
+    k = torch.randn(B, Lk, H, 128, generator=g) * 0.1
+    v = torch.randn(B, Lk, H, 128, generator=g)
+    k[:, Lk - 3] = q[:, 9] * 4.0
+    q, k, v = (t.to(device, torch.bfloat16) for t in (q, k, v))
+    o = N.attn_fwd(q, k, v, n_split=4)
+    assert rel_l2(o, ref_attention(q, k, v)) <= TOL
+
+
+def test_attn_plan_and_bad_split(device):
+    assert N.attn_plan(2, 16, 109120, 109120) >= 1
+    # a grid far below one workgroup per CU (one query block against long keys) is split
+    assert N.attn_plan(1, 1, 256, 109120) > 1
+    q = torch.zeros(1, 64, 1, 128, dtype=torch.bfloat16, device=device)
+    with pytest.raises(ValueError):
+        N.attn_fwd(q, q, q, n_split=2)  # one 64-key tile cannot be split in two

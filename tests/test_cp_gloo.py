@@ -46,6 +46,24 @@ def _worker(rank, world, port, q):
         v = kv[:, :, H:].transpose(0, 1)
         out_loc = sdpa(q_full[:, tok0:tok0 + n], k, v)
         ok_attn = torch.equal(out_loc, ref[:, tok0:tok0 + n])
+        # the device path's pipelined form: K/V packed per head chunk [n*B, 2*Hc*hd], each chunk
+        # all-gathered asynchronously, attention per chunk on the gathered views
+        nc = 2
+        Hc = H // nc
+        kl = k_full[:, tok0:tok0 + n].transpose(0, 1)  # [n, B, H, hd]
+        vl = v_full[:, tok0:tok0 + n].transpose(0, 1)
+        works, alls = [], []
+        for c in range(nc):
+            loc = torch.cat([kl[:, :, c * Hc:(c + 1) * Hc], vl[:, :, c * Hc:(c + 1) * Hc]], 2).reshape(n * B, -1)
+            alls.append(torch.empty((2 * n * B, loc.shape[1]), dtype=loc.dtype))
+            works.append(cpu.all_gather_into_async(alls[c], loc, dist.group.WORLD))
+        ok_chunks = True
+        for c in range(nc):
+            works[c].wait()
+            kc, vc = cpu.kv_chunk_views(alls[c], L, B, Hc, hd)
+            oc = sdpa(q_full[:, tok0:tok0 + n, c * Hc:(c + 1) * Hc], kc, vc)
+            ok_chunks &= torch.equal(oc.view(B, n, Hc, hd), ref.view(B, L, H, hd)[:, tok0:tok0 + n, c * Hc:(c + 1) * Hc])
+        ok_attn = ok_attn and ok_chunks
         # sampler plumbing helpers
         x = torch.arange(L * 3, dtype=torch.float32).view(L, 3)
         ok_split = torch.equal(cpu.split_tokens(x, dist.group.WORLD), x[tok0:tok0 + n])

@@ -2,8 +2,15 @@
 
 Two ranks share cuda:0 (gloo backend; the all-gather of K/V is staged through the host — the RCCL
 path differs only in the transport). Rank r owns tokens [r L/2, (r+1) L/2); the gathered latent must
-match the single-rank run. The only numeric difference is GEMM tiling for M = L/2 vs L (hipBLASLt),
-so the tolerance is rel-L2 <= 5e-3 (guidance 0, 2 Karras steps = 3 evals x CFG).
+match the single-rank run (guidance 0, 2 Karras steps = 3 evals x CFG).
+
+* CP25_ATTN_SPLIT=1 (no key-range split) against CP = 1 run through the same per-batch-entry lanes
+  (`force_lanes`): every attention row sees the same keys in the same order and every GEMM has
+  the same N and K (only M = L/2 vs L), so the two-lane RCCL/gloo pipeline must reproduce CP = 1
+  bit for bit.
+* the production path against the default CP = 1 (one B = 2 pass, library split plan): GEMMs of
+  batch 1 vs 2 and split vs unsplit attention round differently (~1 bf16 ulp per GEMM output,
+  ~2e-3 per forward), amplified over 3 evaluations: rel-L2 <= 1.5e-2.
 """
 import os
 import socket
@@ -33,7 +40,9 @@ def _case():
     cfg = tiny_dit(num_blocks=2)
     sd = {"net." + k: v for k, v in init_state_dict(cfg, seed=3, zero_adaln_out=False).items()}
     g = torch.Generator().manual_seed(30)
-    T, H, W = 3, 16, 32
+    # 768 tokens: 384 per rank and lane, so every GEMM has M >= 384 (hipBLASLt picks a different,
+    # differently-rounding kernel for the MLP's K = 2048 GEMM at M = 192: tools/diag_gemm_m.py)
+    T, H, W = 3, 16, 64
     gt = torch.randn(1, 16, T, H, W, generator=g)
     cc = torch.randn(1, 512, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
     cu = torch.randn(1, 512, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
@@ -46,8 +55,10 @@ def _run(model, gt, cc, cu, shape, dev):
                                 guidance=0.0, seed=0, num_steps=2).cpu()
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, split_env):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if split_env:
+        os.environ["CP25_ATTN_SPLIT"] = split_env
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from cosmos_predict2.model import Video2WorldModelRectifiedFlow
@@ -63,19 +74,25 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_cp2_matches_cp1(device):
+@pytest.mark.parametrize("split_env,tol", [("1", 0.0), ("", 1.5e-2)])
+def test_cp2_matches_cp1(device, monkeypatch, split_env, tol):
     from cosmos_predict2.model import Video2WorldModelRectifiedFlow
 
+    if split_env:
+        monkeypatch.setenv("CP25_ATTN_SPLIT", split_env)
+    else:
+        monkeypatch.delenv("CP25_ATTN_SPLIT", raising=False)
     cfg, scfg, sd, gt, cc, cu, shape = _case()
     m = Video2WorldModelRectifiedFlow(cfg, scfg, device=device)
     m.load_state_dict(sd)
+    m.net.force_lanes = bool(split_env)
     ref = _run(m, gt, cc, cu, shape, device)
     del m
     torch.cuda.empty_cache()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q, split_env)) for r in range(2)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=300) for _ in ps)
@@ -84,5 +101,5 @@ def test_cp2_matches_cp1(device):
     assert all(p.exitcode == 0 for p in ps)
     assert torch.equal(res[0], res[1])  # every rank ends with the full gathered latent
     err = ((res[0] - ref).norm() / ref.norm()).item()
-    print(f"CP=2 vs CP=1 sampler rel-L2: {err:.3e}")
-    assert err <= 5e-3, err
+    print(f"CP=2 vs CP=1 sampler rel-L2 (CP25_ATTN_SPLIT={split_env or 'plan'}): {err:.3e}")
+    assert err <= tol, err

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--fused", action="store_true",
                     help="q/k/v as strided views of a token-major [L, B, 3*H*128] QKV buffer (the DiT's layout)")
     ap.add_argument("--zeros", action="store_true", help="zero-filled inputs (DVFS reference point)")
+    ap.add_argument("--split", type=int, default=0, help="key-range split (0 = the library's plan)")
     ap.add_argument("--lib", default="", help="lab build of libcp25.so to load instead of the in-tree one")
     a = ap.parse_args()
     if a.lib:
@@ -45,20 +46,21 @@ def main():
     if a.zeros:
         for t in (q, k, v):
             t.zero_()
-    o = N.attn_fwd(q, k, v)
+    ns = a.split or N.attn_plan(a.B, a.H, a.L, Lk)
+    o = N.attn_fwd(q, k, v, n_split=ns)
     torch.cuda.synchronize()
     st = torch.cuda.current_stream()
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     e0.record(st)
     for _ in range(a.iters):
-        N.attn_fwd(q, k, v, out=o)
+        N.attn_fwd(q, k, v, out=o, n_split=ns)
     e1.record(st)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
     flop = 4.0 * a.B * a.H * a.L * Lk * 128
     print(json.dumps({"kernel": "attn_fwd", "B": a.B, "H": a.H, "Lq": a.L, "Lk": Lk, "fused": a.fused,
-                      "zeros": a.zeros, "iters": a.iters, "lib": os.path.basename(a.lib) or "libcp25.so", "ms": ms,
+                      "zeros": a.zeros, "split": ns, "iters": a.iters, "lib": os.path.basename(a.lib) or "libcp25.so", "ms": ms,
                       "tflops": flop / ms / 1e9}))
 
 
