@@ -17,6 +17,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -44,6 +45,18 @@ def parse():
     return ap.parse_args()
 
 
+def _heartbeat(rank: int, period: float = 30.0) -> None:
+    """Progress line on stderr every `period` s (a video takes minutes; keeps watchdogs informed)."""
+    t0 = time.time()
+
+    def beat():
+        while True:
+            time.sleep(period)
+            print(f"[bench rank {rank}] running {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -51,6 +64,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}: launch N>1 with torch.distributed.run")
+    _heartbeat(rank)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if world > 1:

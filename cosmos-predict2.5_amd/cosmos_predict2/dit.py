@@ -166,7 +166,6 @@ class MinimalV1LVGDiT:
         self.sd: Dict[str, torch.Tensor] = {}
         self._rope_cache: Dict[Tuple[int, int, int], Tuple[torch.Tensor, torch.Tensor]] = {}
         self.cp_group = None
-        self._lane_streams: List[torch.cuda.Stream] = []  # CP > 1: one stream per CFG batch entry
         self.force_lanes = False  # run the per-batch-entry lanes at CP = 1 too (CP parity tests)
         # optional list collecting (start, end, flop) HIP events around every self-attention launch
         self.attn_events: Optional[list] = None
@@ -288,10 +287,13 @@ class MinimalV1LVGDiT:
         t_B_T: [B, T] fp32, already scaled. Returns the final layer output [n_tok, B, 64] fp32
         (feature order (p1 p2 C) = patch layout).
 
-        CP = 1: one pass over the batch (B = 2 = [cond, uncond]) on the current stream.
-        CP > 1: the batch entries run as two lanes on their own streams, issued block by block in
-        alternation; each lane's self-attention waits for its own K/V all-gather, so one lane's
-        RCCL transfer overlaps the other lane's compute (lane 1 starts half a block behind)."""
+        CP = 1: one pass over the batch (B = 2 = [cond, uncond]).
+        CP > 1: the batch entries run as two software-pipelined lanes on the current stream: each
+        lane yields right after queueing its block's asynchronous RCCL K/V all-gather, and the other
+        lane's whole block is issued before the first lane waits for it, so each transfer runs
+        behind a lane-block of compute (one stream: no cross-stream hazards; a two-stream variant
+        that also ran the lanes' kernels concurrently hung intermittently in device synchronisation
+        on MI355X and was dropped)."""
         cfg = self.cfg
         p = self.sd
         B = ctx.B
@@ -310,50 +312,30 @@ class MinimalV1LVGDiT:
                     next(gen)
                 except StopIteration as e:
                     return e.value
-        cur = torch.cuda.current_stream(self.device)
-        if len(self._lane_streams) < B:
-            self._lane_streams = [torch.cuda.Stream(device=self.device) for _ in range(B)]
-        ready = torch.cuda.Event()
-        ready.record(cur)
-        phase = torch.cuda.Event()
         lanes = []
         for b in range(B):
-            st = self._lane_streams[b]
-            st.wait_event(ready)
             cb = ContextCache(B=1, k=[t[b:b + 1] for t in ctx.k], v=[t[b:b + 1] for t in ctx.v])
             xb = x_in[:, (0 if Bx == 1 else b):(0 if Bx == 1 else b) + 1]
-            with torch.cuda.stream(st):
-                gen = self._blocks(xb, mods[:, :, b:b + 1], shift_f[b:b + 1], scale_f[b:b + 1], cb, geo, cos, sin,
-                                   cp, cp_size, phase_event=phase if b == 0 else None)
-            lanes.append([st, gen, None])
+            lanes.append([self._blocks(xb, mods[:, :, b:b + 1], shift_f[b:b + 1], scale_f[b:b + 1], cb, geo, cos,
+                                       sin, cp, cp_size), None])
         live = B
-        first = True
         while live:
-            for b, lane in enumerate(lanes):
-                if lane[1] is None:
+            for lane in lanes:
+                if lane[0] is None:
                     continue
-                if first and b == 1:
-                    lane[0].wait_event(phase)  # lane 0 recorded it once its first K/V gather was queued
-                with torch.cuda.stream(lane[0]):
-                    try:
-                        next(lane[1])
-                    except StopIteration as e:
-                        lane[2] = e.value
-                        lane[1] = None
-                        live -= 1
-            first = False
-        for st, _, o in lanes:
-            cur.wait_stream(st)
-            o.record_stream(cur)
-        for t in (x_in, mods, shift_f, scale_f, cos, sin):
-            for st, _, _ in lanes:
-                t.record_stream(st)
-        return torch.cat([o for _, _, o in lanes], dim=1)
+                try:
+                    next(lane[0])
+                except StopIteration as e:
+                    lane[1] = e.value
+                    lane[0] = None
+                    live -= 1
+        return torch.cat([o for _, o in lanes], dim=1)
 
-    def _blocks(self, x_in, mods, shift_f, scale_f, ctx: ContextCache, geo: Geometry, cos, sin, cp, cp_size,
-                phase_event=None):
+    def _blocks(self, x_in, mods, shift_f, scale_f, ctx: ContextCache, geo: Geometry, cos, sin, cp, cp_size):
         """Generator: issues the 28 blocks + final layer for the batch entries in x_in/mods/ctx on the
-        current stream, yielding after each block; returns the final layer output [n, B, 64] fp32."""
+        current stream; returns the final layer output [n, B, 64] fp32. Yields (so the caller can
+        issue the other lane) right after each self-attention K/V gather is queued (CP > 1), or after
+        each block (CP = 1)."""
         cfg = self.cfg
         p = self.sd
         B = ctx.B
@@ -393,8 +375,8 @@ class MinimalV1LVGDiT:
                 N.attn_fwd(q, kk, vv, out=o.view(n, B, H, hd).transpose(0, 1), softmax_scale=scale_attn)
                 lk = kk.shape[1]
             else:
-                self._cp_self_attention(i, h, o, cos, sin, n, B, cp, cp_size, ev[0] if ev is not None else None,
-                                        phase_event if i == 0 else None)
+                yield from self._cp_self_attention(i, h, o, cos, sin, n, B, cp, cp_size,
+                                                   ev[0] if ev is not None else None)
                 lk = cp_size * n
             if ev is not None:
                 ev[1].record()
@@ -433,19 +415,19 @@ class MinimalV1LVGDiT:
                 x_new = torch.empty((n, B, D), dtype=BF16, device=self.device)
                 h = N.ln_mod(x, sh, sc, x_st=B * D, x_sb=D, y=y, gate=gate_prev, x_out=x_new, **common)
                 x = x_new
-            yield i
+            if cp is None or cp_size == 1:
+                yield i
         # ---- final layer (fp32 autocast): x + g*y -> LN -> modulate -> Linear(D -> 64)
         xf = N.final_ln_mod(x, shift_f, scale_f, y=y, gate=gate_prev, **common)
         out = F.linear(xf.view(n * B, D), self.w_final)
         return out.view(n, B, -1)
 
     def _cp_self_attention(self, i: int, h: torch.Tensor, o: torch.Tensor, cos, sin, n: int, B: int, cp,
-                           cp_size: int, e0=None, phase_event=None) -> None:
+                           cp_size: int, e0=None):
         """Self-attention of a context-parallel token shard (replaces the reference's Ulysses
         all-to-all, a2a_cp.py:160-219, which needs T % cp == 0): the shard's normed + roped K|V rows
         are all-gathered from every rank over RCCL, asynchronously (the other lane computes
-        meanwhile); the attention waits for the gather only. The launch is unsplit: the two lanes'
-        kernels run concurrently and fill each other's tails. Same QKV GEMM and norm as CP = 1."""
+        meanwhile); the attention waits for the gather only. Same QKV GEMM and norm as CP = 1."""
         cfg = self.cfg
         p = self.sd
         pre = f"blocks.{i}."
@@ -457,8 +439,7 @@ class MinimalV1LVGDiT:
         N.copy_rows(qkv, 3 * D, kv, 2 * D, n * B, 2 * D, src_offset=D)
         kv_all = torch.empty((cp_size * n * B, 2 * D), dtype=BF16, device=self.device)
         work = all_gather_into_async(kv_all, kv, cp)  # RCCL over xGMI
-        if phase_event is not None:
-            phase_event.record()
+        yield i  # the other lane's block runs here (in issue order) while this gather is in flight
         N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=0, weight=p[pre + "self_attn.q_norm.weight"],
                             cos=cos, sin=sin)
         work.wait()
@@ -466,7 +447,8 @@ class MinimalV1LVGDiT:
             e0.record()
         kc, vc = kv_chunk_views(kv_all, cp_size * n, B, H, hd)
         q = qkv.view(n, B, 3 * D)[:, :, :D].view(n, B, H, hd).transpose(0, 1)
-        N.attn_fwd(q, kc, vc, out=o.view(n, B, H, hd).transpose(0, 1), softmax_scale=hd ** -0.5, n_split=1)
+        # the library's key-range split plan: B = 1 launches at CP = 8 leave a ragged last round
+        N.attn_fwd(q, kc, vc, out=o.view(n, B, H, hd).transpose(0, 1), softmax_scale=hd ** -0.5)
 
     # ---------------------------------------------------------------- reference-compatible forward
     @torch.no_grad()
