@@ -44,9 +44,11 @@ def all_gather_into(out: torch.Tensor, x: torch.Tensor, group) -> torch.Tensor:
         xc = x.detach().contiguous().cpu()
         parts = [torch.empty_like(xc) for _ in range(w)]
         dist.all_gather(parts, xc, group=group)
-        out.copy_(torch.cat(parts, 0))
+        out.view((w * xc.shape[0],) + tuple(xc.shape[1:])).copy_(torch.cat(parts, 0))
         return out
-    dist.all_gather_into_tensor(out, x.contiguous(), group=group)
+    w = dist.get_world_size(group)
+    # the concatenated [w * x0, ...] form (every backend accepts it; out may be given stacked)
+    dist.all_gather_into_tensor(out.view((w * x.shape[0],) + tuple(x.shape[1:])), x.contiguous(), group=group)
     return out
 
 
@@ -65,7 +67,9 @@ def all_gather_into_async(out: torch.Tensor, x: torch.Tensor, group):
     if dist.get_backend(group) == "gloo" and x.is_cuda:
         all_gather_into(out, x, group)
         return _Done()
-    return dist.all_gather_into_tensor(out, x.contiguous(), group=group, async_op=True)
+    w = dist.get_world_size(group)
+    return dist.all_gather_into_tensor(out.view((w * x.shape[0],) + tuple(x.shape[1:])), x.contiguous(),
+                                       group=group, async_op=True)
 
 
 def kv_chunk_views(kv_all_c: torch.Tensor, n_tok_total: int, B: int, Hc: int, hd: int):

@@ -64,6 +64,8 @@ class Video2WorldModelRectifiedFlow:
 
     def set_context_parallel_group(self, group) -> None:
         self.cp_group = group
+        if self.tokenizer is not None and hasattr(self.tokenizer, "set_context_parallel_group"):
+            self.tokenizer.set_context_parallel_group(group)
         if group is None:
             self.net.disable_context_parallel()
         else:

@@ -12,6 +12,16 @@ re-laid-out for the GPU:
   its epilogue, bias + residual adds into the conv epilogue; RMS_norm + SiLU is one HIP kernel.
 The single-head AttentionBlock core (C = 384 at h/8 x w/8) runs as two fp32 GEMMs + softmax on the
 device (round-1 interim; its 1x1 projections and norm are the HIP kernels).
+
+Context parallel decode (set_context_parallel_group): the reference replicates the VAE on every rank;
+here each rank decodes a band of h/N latent rows (8h/N output rows) of every frame. A 3x3 conv needs
+one input row beyond its band on each side: `_halo` fetches the neighbours' edge rows (RCCL
+all-gather of the bands' first/last rows; zero rows at the image edge = the conv's zero padding)
+and the conv runs unpadded in h over the haloed band (causal caches keep the haloed frames, so the
+cached frames carry their halos too); the nearest-2x upsample conv reads the haloed low-res band with
+pads (-1, -1), the (3,1,1) time_conv and 1x1 convs need no halo, RMS_norm is per pixel, and the
+middle AttentionBlock gathers K/V of the whole frame. Bands are gathered into the full video at the
+end. Every output pixel is computed from the same inputs in the same order as the unbanded decode.
 """
 from __future__ import annotations
 
@@ -22,6 +32,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _native as N
+from . import context_parallel as cpx
 
 BF16 = torch.bfloat16
 CACHE_T = 2
@@ -201,11 +212,38 @@ class WanVAE:
         mean = torch.tensor(_MEAN, dtype=BF16, device=self.device)
         std = torch.tensor(_STD, dtype=BF16, device=self.device)
         self.mean, self.inv_std = mean, 1.0 / std
+        self.cp_group = None  # decode shards latent rows over this group (see module docstring)
+        self._band = None  # (group, rank, world) while a banded decode runs
+
+    # ---------------------------------------------------------------- context-parallel bands
+    def _halo(self, x: torch.Tensor) -> torch.Tensor:
+        """[T, R, W, C] band -> [T, R + 2, W, C] with the neighbouring bands' edge rows (zeros at the
+        image's top and bottom edge)."""
+        group, r, n = self._band
+        T, R, W, C = x.shape
+        xh = torch.empty((T, R + 2, W, C), dtype=x.dtype, device=x.device)
+        xh[:, 1:R + 1] = x
+        edge = torch.stack([x[:, 0], x[:, R - 1]], 0)  # [2, T, W, C]
+        allv = torch.empty((n,) + tuple(edge.shape), dtype=x.dtype, device=x.device)
+        cpx.all_gather_into(allv, edge, group)
+        if r > 0:
+            xh[:, 0] = allv[r - 1, 1]
+        else:
+            xh[:, 0].zero_()
+        if r < n - 1:
+            xh[:, R + 1] = allv[r + 1, 0]
+        else:
+            xh[:, R + 1].zero_()
+        return xh
 
     # ---------------------------------------------------------------- building blocks
     def _causal(self, name, x, cache: Optional[_FeatCache], H, W):
         """CausalConv3d 3x3x3 (pad 1) with the feat_cache rule (wan2pt1.py:206-219)."""
         conv = self.convs[name]
+        pad = (1, 1, 1, 1)
+        if self._band is not None:
+            x = self._halo(x)
+            H, pad = H + 2, (0, 1, 0, 1)
         T = x.shape[0]
         prev = None
         if cache is not None:
@@ -219,7 +257,7 @@ class WanVAE:
         pre: List[Optional[torch.Tensor]] = [None, None]
         if prev is not None:
             pre = [None] * (2 - prev.shape[0]) + _frames(prev)
-        return conv(pre + _frames(x), T, H, W, pad=(1, 1, 1, 1))
+        return conv(pre + _frames(x), T, H, W, pad=pad)
 
     def _res(self, p, x, cache, H, W, cin, cout):
         if cin != cout:
@@ -233,6 +271,10 @@ class WanVAE:
 
     def _causal_res(self, name, x, cache, H, W, residual=None):
         conv = self.convs[name]
+        pad = (1, 1, 1, 1)
+        if self._band is not None:
+            x = self._halo(x)
+            H, pad = H + 2, (0, 1, 0, 1)
         T = x.shape[0]
         i = cache.idx
         prev = cache.slots.get(i)
@@ -242,7 +284,7 @@ class WanVAE:
         cache.slots[i] = cache_x
         cache.idx += 1
         pre: List[Optional[torch.Tensor]] = [None, None] if prev is None else [None] * (2 - prev.shape[0]) + _frames(prev)
-        return conv(pre + _frames(x), T, H, W, pad=(1, 1, 1, 1), residual=residual)
+        return conv(pre + _frames(x), T, H, W, pad=pad, residual=residual)
 
     def _attn(self, p, x, H, W):
         C = x.shape[-1]
@@ -251,8 +293,17 @@ class WanVAE:
         qkv = self.convs[p + ".to_qkv"](_frames(y), T, H, W)  # [T, H, W, 3C]
         qkv = qkv.view(T, H * W, 3 * C)
         o = torch.empty((T, H * W, C), dtype=BF16, device=self.device)
+        kv_all = None
+        if self._band is not None:  # K/V of the whole frame: every band's rows, in row order
+            group, _, n = self._band
+            kv = qkv[:, :, C:].contiguous()
+            kv_all = torch.empty((n,) + tuple(kv.shape), dtype=BF16, device=self.device)
+            cpx.all_gather_into(kv_all, kv, group)
         for t in range(T):
             q, k, v = qkv[t, :, :C].float(), qkv[t, :, C:2 * C].float(), qkv[t, :, 2 * C:].float()
+            if kv_all is not None:
+                k = kv_all[:, t, :, :C].reshape(-1, C).float()
+                v = kv_all[:, t, :, C:].reshape(-1, C).float()
             s = torch.matmul(q, k.t()) * (C ** -0.5)
             o[t] = torch.matmul(torch.softmax(s, -1), v).to(BF16)
         o = o.view(T, H, W, C)
@@ -278,7 +329,12 @@ class WanVAE:
                 cache.idx += 1
         T = x.shape[0]
         conv = self.convs[p + ".resample.1"]
-        if kind.startswith("upsample"):
+        if kind.startswith("upsample") and self._band is not None:
+            # haloed low-res band; in upsampled coordinates the output rows start one row in: pads -1
+            xh = self._halo(x)
+            y = conv(_frames(xh), T, H + 2, W, pad=(-1, 1, -1, 1), upsample=True)
+            H, W = 2 * H, 2 * W
+        elif kind.startswith("upsample"):
             y = conv(_frames(x), T, H, W, pad=(1, 1, 1, 1), upsample=True)
             H, W = 2 * H, 2 * W
         else:
@@ -362,14 +418,27 @@ class WanVAE:
         _, C, T, h, w = z.shape
         zl = z[0].to(self.device, BF16).permute(1, 2, 3, 0).contiguous()  # [T, h, w, 16]
         zl = zl / self.inv_std + self.mean
-        x = self.convs["conv2"](_frames(zl.contiguous()), T, h, w)
-        cache = _FeatCache()
-        outs = []
-        for i in range(T):
-            cache.idx = 0
-            o, H, W = self._decoder(x[i: i + 1].contiguous(), cache, h, w)
-            outs.append(o)
-        video = torch.cat(outs, 0)  # [Tp, H, W, 3]
+        group = self.cp_group
+        r, n = cpx.cp_rank_world(group)
+        if n > 1 and h % n == 0:
+            self._band = (group, r, n)
+            zl = zl[:, r * (h // n):(r + 1) * (h // n)]
+            h = h // n
+        try:
+            x = self.convs["conv2"](_frames(zl.contiguous()), T, h, w)
+            cache = _FeatCache()
+            outs = []
+            for i in range(T):
+                cache.idx = 0
+                o, H, W = self._decoder(x[i: i + 1].contiguous(), cache, h, w)
+                outs.append(o)
+            video = torch.cat(outs, 0)  # [Tp, H, W, 3] (this rank's band of H rows when banded)
+            if self._band is not None:
+                allv = torch.empty((n,) + tuple(video.shape), dtype=video.dtype, device=video.device)
+                cpx.all_gather_into(allv, video, group)
+                video = allv.permute(1, 0, 2, 3, 4).reshape(video.shape[0], n * video.shape[1], *video.shape[2:])
+        finally:
+            self._band = None
         return video.permute(3, 0, 1, 2).unsqueeze(0).contiguous()
 
 
@@ -380,6 +449,10 @@ class Wan2pt1VAEInterface:
                  chunk_duration: int = 81):
         self.model = WanVAE(state_dict, device=device, temporal_window=temporal_window)
         self.chunk_duration = chunk_duration
+
+    def set_context_parallel_group(self, group) -> None:
+        """Decode shards latent rows over `group` (WanVAE module docstring); encode stays replicated."""
+        self.model.cp_group = group
 
     def encode(self, state: torch.Tensor) -> torch.Tensor:
         in_dtype = state.dtype

@@ -71,7 +71,17 @@ def _worker(rank, world, port, q):
         b = torch.full((2, 3), float(rank)) if rank == 0 else torch.empty(0)
         b = cpu.broadcast(b, dist.group.WORLD)
         ok_bcast = b.shape == (2, 3) and torch.all(b == 0).item()
-        q.put((rank, ok_attn, ok_split, ok_gather, ok_bcast))
+        # VAE decode bands: the halo rows of a band are its neighbours' edge rows, zeros at the edges
+        from cosmos_predict2.vae import WanVAE
+
+        full = torch.arange(2 * 8 * 3 * 4, dtype=torch.float32).view(2, 8, 3, 4)  # [T, h, w, C]
+        vae = WanVAE.__new__(WanVAE)
+        vae._band = (dist.group.WORLD, rank, 2)
+        band = full[:, rank * 4:(rank + 1) * 4].contiguous()
+        hal = vae._halo(band)
+        padded = torch.cat([torch.zeros(2, 1, 3, 4), full, torch.zeros(2, 1, 3, 4)], 1)
+        ok_halo = torch.equal(hal, padded[:, rank * 4:rank * 4 + 6])
+        q.put((rank, ok_attn, ok_split, ok_gather, ok_bcast, ok_halo))
     finally:
         dist.destroy_process_group()
 

@@ -95,7 +95,7 @@ def test_cp2_matches_cp1(device, monkeypatch, split_env, tol):
     ps = [ctx.Process(target=_worker, args=(r, 2, port, q, split_env)) for r in range(2)]
     for p in ps:
         p.start()
-    res = {r: torch.from_numpy(a) for r, a in (q.get(timeout=300) for _ in ps)}
+    res = {r: torch.from_numpy(a) for r, a in (q.get(timeout=100) for _ in ps)}
     for p in ps:
         p.join(timeout=120)
     assert all(p.exitcode == 0 for p in ps)
