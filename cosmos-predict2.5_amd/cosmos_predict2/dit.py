@@ -69,6 +69,13 @@ def state_dict_shapes(cfg: DiTConfig) -> Dict[str, Tuple[Tuple[int, ...], torch.
         for m in ("self_attn", "cross_attn", "mlp"):
             s[p + f"adaln_modulation_{m}.1.weight"] = ((A, D), BF16)
             s[p + f"adaln_modulation_{m}.2.weight"] = ((3 * D, A), BF16)
+    if cfg.action_dim:
+        fin, hid = cfg.action_in_features, cfg.action_hidden_features
+        for name, out in (("action_embedder_B_D", D), ("action_embedder_B_3D", 3 * D)):
+            s[name + ".fc1.weight"] = ((hid, fin), BF16)
+            s[name + ".fc1.bias"] = ((hid,), BF16)
+            s[name + ".fc2.weight"] = ((out, hid), BF16)
+            s[name + ".fc2.bias"] = ((out,), BF16)
     return s
 
 
@@ -85,7 +92,9 @@ def init_state_dict(cfg: DiTConfig, seed: int = 0, device="cpu", zero_adaln_out:
         return t.to(BF16)
 
     D = cfg.model_channels
-    for name, (shape, _) in state_dict_shapes(cfg).items():
+    shapes = state_dict_shapes(cfg)
+    shapes_fan = {k: shapes[k[: k.rindex(".")] + ".weight"][0][1] for k in shapes if k.startswith("action_embedder")}
+    for name, (shape, _) in shapes.items():
         if name.endswith("norm.weight"):
             out[name] = torch.ones(shape, dtype=BF16, device=device)
         elif name == "pos_embedder.seq":
@@ -93,6 +102,10 @@ def init_state_dict(cfg: DiTConfig, seed: int = 0, device="cpu", zero_adaln_out:
         elif name.startswith("pos_embedder.dim_"):
             full = 2 * shape[0] if "spatial" in name else 2 * shape[0]
             out[name] = (torch.arange(0, full, 2, device=device)[: shape[0]].float() / full).to(BF16)
+        elif name.startswith("action_embedder"):  # nn.Linear default init (not covered by init_weights)
+            fan_in = shapes_fan[name]
+            bound = 1.0 / math.sqrt(fan_in)
+            out[name] = (torch.rand(shape, generator=g, device=device) * 2 - 1).mul_(bound).to(BF16)
         elif name.startswith("crossattn_proj"):
             bound = 1.0 / math.sqrt(cfg.crossattn_proj_in_channels)
             out[name] = (torch.rand(shape, generator=g, device=device) * 2 - 1).mul_(bound).to(BF16)
@@ -253,9 +266,46 @@ class MinimalV1LVGDiT:
 
     # ---------------------------------------------------------------- fp32 conditioning
     @torch.no_grad()
-    def time_modulation(self, t_B_T: torch.Tensor):
+    def action_embedding(self, action: torch.Tensor, B: int, T: int):
+        """Action-conditioned nets: action [B' (1 or B), A, action_dim] -> (emb_D [B, T|1, D],
+        emb_3D [B, T|1, 3D]) bf16, the reference's bf16 Mlp (fc1 + bias, GELU tanh, fc2 + bias)
+        (action_conditioned_minimal_v1_lvg_dit.py:28-45, per-chunk :104-107, per-latent-frame
+        :257-270 with a zero embedding for latent frame 0)."""
+        cfg = self.cfg
+        p = self.sd
+        a = action.to(device=self.device, dtype=BF16)
+        Ba, A, dim = a.shape
+        if dim != cfg.action_dim:
+            raise ValueError(f"action_dim {dim} != the net's {cfg.action_dim}")
+        if cfg.action_per_latent_frame:
+            per = cfg.action_per_latent_frame
+            if A % per or A // per + 1 != T:
+                raise ValueError(f"{A} actions do not give {T - 1} latent frames of {per}")
+            a = a.reshape(Ba, A // per, per * dim)
+        else:
+            if A != cfg.num_action_per_chunk:
+                raise ValueError(f"{A} actions, the net takes {cfg.num_action_per_chunk} per chunk")
+            a = a.reshape(Ba, 1, A * dim)
+
+        def mlp(name):
+            h = F.linear(a, p[name + ".fc1.weight"], p[name + ".fc1.bias"])
+            h = F.gelu(h, approximate="tanh")
+            return F.linear(h, p[name + ".fc2.weight"], p[name + ".fc2.bias"])
+
+        e_d, e_3d = mlp("action_embedder_B_D"), mlp("action_embedder_B_3D")
+        if cfg.action_per_latent_frame:
+            e_d = torch.cat([torch.zeros_like(e_d[:, :1]), e_d], 1)
+            e_3d = torch.cat([torch.zeros_like(e_3d[:, :1]), e_3d], 1)
+        if Ba != B:
+            e_d, e_3d = e_d.expand(B, -1, -1), e_3d.expand(B, -1, -1)
+        return e_d, e_3d
+
+    @torch.no_grad()
+    def time_modulation(self, t_B_T: torch.Tensor, action: Optional[torch.Tensor] = None):
         """t (already * timestep_scale) [B, T] fp32 -> (block mods bf16 [nb, 3, B, T, 3D],
-        final shift/scale fp32 [B, T, D] each). fp32 math (use_wan_fp32_strategy)."""
+        final shift/scale fp32 [B, T, D] each). fp32 math (use_wan_fp32_strategy). Action nets add
+        the action embeddings to the embedding and the AdaLN-LoRA term before the norm
+        (action_conditioned_minimal_v1_lvg_dit.py:298-305)."""
         cfg = self.cfg
         p = self.sd
         D = cfg.model_channels
@@ -267,6 +317,14 @@ class MinimalV1LVGDiT:
         sincos = torch.cat([torch.cos(arg), torch.sin(arg)], dim=-1).view(B, T, D)
         h = F.silu(F.linear(sincos, p["t_embedder.1.linear_1.weight"].float()))
         lora = F.linear(h, p["t_embedder.1.linear_2.weight"].float())  # [B, T, 3D]
+        if cfg.action_dim:
+            if action is None:
+                raise ValueError("this action-conditioned net needs `action`")
+            e_d, e_3d = self.action_embedding(action, B, T)
+            sincos = sincos + e_d.float()
+            lora = lora + e_3d.float()
+        elif action is not None:
+            raise ValueError("`action` given to a net without action embedders")
         xf = sincos
         emb = ((xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-6)) * p["t_embedding_norm.weight"].float())
         se = F.silu(emb)  # [B, T, D]
@@ -282,7 +340,7 @@ class MinimalV1LVGDiT:
     # ---------------------------------------------------------------- hot path
     @torch.no_grad()
     def forward_tokens(self, patch_rows: torch.Tensor, t_B_T: torch.Tensor, ctx: ContextCache,
-                       geo: Geometry) -> torch.Tensor:
+                       geo: Geometry, action: Optional[torch.Tensor] = None) -> torch.Tensor:
         """patch_rows: [n_tok, Bx, 72] bf16 (Bx = 1 shares the input across the CFG batch);
         t_B_T: [B, T] fp32, already scaled. Returns the final layer output [n_tok, B, 64] fp32
         (feature order (p1 p2 C) = patch layout).
@@ -301,7 +359,7 @@ class MinimalV1LVGDiT:
         n = geo.n_tok
         Bx = patch_rows.shape[1]
         x_in = F.linear(patch_rows.reshape(n * Bx, -1), p["x_embedder.proj.1.weight"]).view(n, Bx, D)
-        mods, shift_f, scale_f = self.time_modulation(t_B_T)
+        mods, shift_f, scale_f = self.time_modulation(t_B_T, action)
         cos, sin = self.rope_tables(geo)
         cp = self.cp_group
         cp_size = 1 if cp is None else torch.distributed.get_world_size(cp)
@@ -454,8 +512,10 @@ class MinimalV1LVGDiT:
     @torch.no_grad()
     def forward(self, x_B_C_T_H_W: torch.Tensor, timesteps_B_T: torch.Tensor, crossattn_emb: torch.Tensor,
                 condition_video_input_mask_B_C_T_H_W: Optional[torch.Tensor] = None, fps=None,
-                padding_mask: Optional[torch.Tensor] = None, data_type=None, **kwargs) -> torch.Tensor:
-        """MinimalV1LVGDiT.forward signature (minimal_v1_lvg_dit.py:31-62) -> [B, C, T, H, W] fp32."""
+                padding_mask: Optional[torch.Tensor] = None, data_type=None, action: Optional[torch.Tensor] = None,
+                **kwargs) -> torch.Tensor:
+        """MinimalV1LVGDiT.forward signature (minimal_v1_lvg_dit.py:31-62; action nets:
+        action_conditioned_minimal_v1_lvg_dit.py:236-249) -> [B, C, T, H, W] fp32."""
         cfg = self.cfg
         B, C, T, Hl, Wl = x_B_C_T_H_W.shape
         Hp, Wp = Hl // cfg.patch_spatial, Wl // cfg.patch_spatial
@@ -479,7 +539,7 @@ class MinimalV1LVGDiT:
         t = timesteps_B_T.to(self.device).float() * cfg.timestep_scale
         if t.shape[1] == 1 and T > 1:
             t = t.expand(B, T).contiguous()
-        out = self.forward_tokens(rows.contiguous(), t, ctx, geo)  # [L, B, 64] (p1 p2 C)
+        out = self.forward_tokens(rows.contiguous(), t, ctx, geo, action=action)  # [L, B, 64] (p1 p2 C)
         out = out.view(T, Hp, Wp, B, 2, 2, C).permute(3, 6, 0, 1, 4, 2, 5)
         return out.reshape(B, C, T, Hl, Wl).float()
 

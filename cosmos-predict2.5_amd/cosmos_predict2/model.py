@@ -100,7 +100,7 @@ class Video2WorldModelRectifiedFlow:
     def sample_latents(self, gt: Optional[torch.Tensor], ctx_cond: torch.Tensor, ctx_uncond: torch.Tensor, *,
                        state_shape, num_conditional_frames: int, guidance: float, seed: int, num_steps: int,
                        shift: float = 5.0, cfg_mode: Optional[str] = None, progress=None,
-                       net_fn=None) -> torch.Tensor:
+                       net_fn=None, action: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Core loop. gt: x0 latent [1, C, T, H, W] fp32 (or None when no frame is conditioned);
         ctx_*: text embeddings [1, Lctx, proj_in]. Returns latents [1, C, T, H, W] fp32.
         net_fn(rows [n,1,72] bf16, t_B_T [2,T] fp32, geo) -> [n,2,64] replaces the DiT (tests only)."""
@@ -139,7 +139,7 @@ class Video2WorldModelRectifiedFlow:
             tf = self._frame_timesteps(t, frame_mask)  # [T]
             t_B_T = (tf[None, :] * scale).expand(2, T).contiguous()
             if net_fn is None:
-                net_out = self.net.forward_tokens(rows.view(geo.n_tok, 1, -1), t_B_T, ctx, geo)
+                net_out = self.net.forward_tokens(rows.view(geo.n_tok, 1, -1), t_B_T, ctx, geo, action=action)
             else:
                 net_out = net_fn(rows.view(geo.n_tok, 1, -1), t_B_T, geo)
             v = N.cfg_velocity(net_out, noise, gtp, frame_mask, guidance, mode, tok0=geo.tok0, hw=geo.hw)
@@ -172,8 +172,11 @@ class Video2WorldModelRectifiedFlow:
             ctx_u = data_batch["neg_t5_text_embeddings"]
         else:
             ctx_u = torch.zeros_like(ctx_c)  # TextAttr dropout (rate 0.2 > 0) zeroes the embedding
+        # action-conditioned nets: the same action conditions both CFG branches (the conditioner's
+        # action ReMapkey has no dropout: action/configs/action_conditioned/conditioner.py:222-233,272-275)
         return self.sample_latents(gt, ctx_c, ctx_u, state_shape=state_shape, num_conditional_frames=n_cond,
-                                   guidance=guidance, seed=seed, num_steps=num_steps, shift=shift)
+                                   guidance=guidance, seed=seed, num_steps=num_steps, shift=shift,
+                                   action=data_batch.get("action"))
 
     @torch.no_grad()
     def encode_conditioning(self, video: torch.Tensor, n_cond: int, T_lat: int) -> torch.Tensor:

@@ -39,6 +39,16 @@ class DiTConfig:
     rope_enable_fps_modulation: bool = False
     timestep_scale: float = 0.001
     use_wan_fp32_strategy: bool = True
+    # action conditioning (cosmos_predict2/_src/predict2/action/networks/action_conditioned_minimal_v1_lvg_dit.py):
+    # action_dim > 0 adds action_embedder_B_D / _B_3D (Linear-GELU(tanh)-Linear MLPs) whose outputs are
+    # added to the timestep embedding and the AdaLN-LoRA term before t_embedding_norm.
+    action_dim: int = 0
+    # > 0: ActionChunkConditionedMinimalV1LVGDiT (:182-346): actions grouped per latent frame
+    # (temporal_compression_ratio of them), latent frame 0 gets a zero embedding;
+    # 0: ActionConditionedMinimalV1LVGDiT (:48-179): one embedding of the whole chunk for every frame
+    action_per_latent_frame: int = 0
+    num_action_per_chunk: int = 12
+    action_hidden: int = 0  # hidden width of the embedder MLPs (0 = 4 * model_channels)
 
     @property
     def head_dim(self) -> int:
@@ -52,6 +62,15 @@ class DiTConfig:
     @property
     def mlp_hidden(self) -> int:
         return int(self.model_channels * self.mlp_ratio)
+
+    @property
+    def action_in_features(self) -> int:
+        per = self.action_per_latent_frame or self.num_action_per_chunk
+        return self.action_dim * per
+
+    @property
+    def action_hidden_features(self) -> int:
+        return self.action_hidden or 4 * self.model_channels
 
     def replace(self, **kw) -> "DiTConfig":
         return dataclasses.replace(self, **kw)
@@ -76,12 +95,20 @@ DIT_14B = DiTConfig(model_channels=5120, num_heads=40, num_blocks=36)
 
 SAMPLER_2B_POST_TRAINED = SamplerConfig(use_kerras_sigma_at_inference=True, conditional_frame_timestep=0.1)
 SAMPLER_PRE_TRAINED = SamplerConfig()
+# robot/action-cond (checkpoint_db.py:469-492, experiment ..._action_conditioned_rectified_flow_bridge_13frame_256x320,
+# exp_2B_action_conditioned_rectify_flow.py:617-657): ActionChunk net, action_dim 7, 4 actions per latent
+# frame, state_t = 1 + 12 // 4 = 4 (13 frames at 256x320), shift-5 linspace schedule, no conditional-frame
+# timestep; the 2B net's rope / timestep / crossattn overrides of the base rectified-flow experiment
+# (:308-320) apply on top of the /net group default.
+DIT_2B_ACTION = DIT_2B.replace(action_dim=7, action_per_latent_frame=4)
+SAMPLER_ACTION = SamplerConfig(state_t=4, resolution="256")
 
 # model name (cosmos_predict2/config.py ModelKey.name) -> (net, sampler)
 MODELS = {
     "2B/post-trained": (DIT_2B, SAMPLER_2B_POST_TRAINED),
     "2B/pre-trained": (DIT_2B, SAMPLER_PRE_TRAINED),
     "14B/pre-trained": (DIT_14B, SAMPLER_PRE_TRAINED),
+    "2B/robot/action-cond": (DIT_2B_ACTION, SAMPLER_ACTION),
 }
 
 # Subset of VIDEO_RES_SIZE_INFO (cosmos_predict2/_src/predict2/datasets/utils.py:44-67); the model's

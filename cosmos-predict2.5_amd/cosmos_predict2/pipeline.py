@@ -40,11 +40,12 @@ DEFAULT_NEGATIVE_PROMPT = (
 TEXT_EMB_SHAPE = (1, 512, 100352)
 
 
-def synthetic_text_encoder(prompt: str, device="cuda") -> torch.Tensor:
+def synthetic_text_encoder(prompt: str, device="cuda", dim: int = TEXT_EMB_SHAPE[2]) -> torch.Tensor:
     """Deterministic N(0, 1) embedding per prompt (matches the mean-normalized Reason1 layer stats)."""
     seed = int.from_bytes(hashlib.sha256(prompt.encode()).digest()[:4], "little")
     g = torch.Generator(device=device).manual_seed(seed)
-    return torch.randn(TEXT_EMB_SHAPE, generator=g, device=device, dtype=torch.float32).to(torch.bfloat16)
+    shape = TEXT_EMB_SHAPE[:2] + (dim,)
+    return torch.randn(shape, generator=g, device=device, dtype=torch.float32).to(torch.bfloat16)
 
 
 def resize_input(video: torch.Tensor, resolution) -> torch.Tensor:
@@ -137,7 +138,8 @@ class Video2WorldInference:
         del sd
         if self.process_group is not None:
             self.model.set_context_parallel_group(self.process_group)
-        self.text_encoder = text_encoder or (lambda p: synthetic_text_encoder(p, self.device))
+        emb_dim = ncfg.crossattn_proj_in_channels if ncfg.use_crossattn_projection else ncfg.crossattn_emb_channels
+        self.text_encoder = text_encoder or (lambda p: synthetic_text_encoder(p, self.device, emb_dim))
         self.batch_size = 1
 
     def _init_distributed(self):
@@ -154,7 +156,8 @@ class Video2WorldInference:
         self.process_group = groups[rank // cp]
 
     def _get_data_batch_input(self, video: torch.Tensor, prompt: str, num_conditional_frames: int = 1,
-                              negative_prompt: str = DEFAULT_NEGATIVE_PROMPT, use_neg_prompt: bool = True):
+                              negative_prompt: str = DEFAULT_NEGATIVE_PROMPT, use_neg_prompt: bool = True,
+                              action: Optional[torch.Tensor] = None):
         B, C, T, H, W = video.shape
         batch = {
             "dataset_name": "video_data",
@@ -166,6 +169,8 @@ class Video2WorldInference:
         }
         if use_neg_prompt:
             batch["neg_t5_text_embeddings"] = self.text_encoder(negative_prompt)
+        if action is not None:  # video2world.py:352: action.unsqueeze(0) -> [1, A, action_dim]
+            batch["action"] = action.unsqueeze(0) if action.dim() == 2 else action
         for k, v in batch.items():
             if isinstance(v, torch.Tensor) and torch.is_floating_point(v):
                 batch[k] = v.to(self.device, torch.bfloat16)
@@ -175,8 +180,9 @@ class Video2WorldInference:
     def generate_vid2world(self, prompt: str, input_path=None, guidance: int = 7, num_video_frames: int = 77,
                            num_latent_conditional_frames: int = 1, resolution: str = "192,320", seed: int = 1,
                            negative_prompt: str = DEFAULT_NEGATIVE_PROMPT, num_steps: int = 35,
-                           **unused) -> torch.Tensor:
-        """-> video [1, 3, T, H, W] in [-1, 1] (fp32). T = tokenizer.get_pixel_num_frames(state_t) (F5)."""
+                           action: Optional[torch.Tensor] = None, **unused) -> torch.Tensor:
+        """-> video [1, 3, T, H, W] in [-1, 1] (fp32). T = tokenizer.get_pixel_num_frames(state_t) (F5).
+        action: [A, action_dim] for the action-conditioned model (video2world.py:325-352)."""
         if resolution == "none":
             h, w = VIDEO_RES_SIZE_INFO[self.model.config.resolution]["9,16"]
         else:
@@ -198,7 +204,8 @@ class Video2WorldInference:
         import time
 
         t0 = time.perf_counter()
-        batch = self._get_data_batch_input(vid, prompt, num_latent_conditional_frames, negative_prompt)
+        batch = self._get_data_batch_input(vid, prompt, num_latent_conditional_frames, negative_prompt,
+                                           action=action)
         latents = self.model.generate_samples_from_batch(batch, guidance=guidance, seed=seed, is_negative_prompt=True,
                                                          num_steps=num_steps)
         torch.cuda.synchronize(self.device)

@@ -102,8 +102,29 @@ def _lin(x, w, b=None):
     return F.linear(x, w, b)
 
 
-def timestep_embedding(cfg, sd, t_B_T: torch.Tensor):
-    """Timesteps + TimestepEmbedding(adaln-lora) + t_embedding_norm, fp32 (autocast)."""
+def action_embedding(cfg, sd, action: torch.Tensor):
+    """action_conditioned_minimal_v1_lvg_dit.py: Mlp (:28-45: fc1 + bias, GELU(tanh), fc2 + bias) in
+    the model dtype (bf16) on the action [B, A, d]; per chunk (:104-107) -> [B, 1, *], per latent
+    frame (:257-270) -> [B, A/r, *] with a zero row prepended for latent frame 0."""
+    a = action.to(BF16)
+    B, A, d = a.shape
+    r = cfg.get("action_per_latent_frame", 0)
+    a = a.reshape(B, A // r, r * d) if r else a.reshape(B, 1, A * d)
+
+    def mlp(name):
+        h = F.gelu(_lin(a, _w(sd, name + ".fc1.weight"), _w(sd, name + ".fc1.bias")), approximate="tanh")
+        return _lin(h, _w(sd, name + ".fc2.weight"), _w(sd, name + ".fc2.bias"))
+
+    e_d, e_3d = mlp("action_embedder_B_D"), mlp("action_embedder_B_3D")
+    if r:
+        e_d = torch.cat([torch.zeros_like(e_d[:, :1]), e_d], 1)
+        e_3d = torch.cat([torch.zeros_like(e_3d[:, :1]), e_3d], 1)
+    return e_d, e_3d
+
+
+def timestep_embedding(cfg, sd, t_B_T: torch.Tensor, action: torch.Tensor | None = None):
+    """Timesteps + TimestepEmbedding(adaln-lora) + t_embedding_norm, fp32 (autocast); action nets add
+    the action embeddings before the norm (action_conditioned_minimal_v1_lvg_dit.py:298-305)."""
     D = cfg["model_channels"]
     half = D // 2
     expo = -math.log(10000) * torch.arange(half, dtype=F32) / (half - 0.0)
@@ -111,6 +132,10 @@ def timestep_embedding(cfg, sd, t_B_T: torch.Tensor):
     sincos = torch.cat([torch.cos(emb), torch.sin(emb)], dim=-1).reshape(t_B_T.shape[0], t_B_T.shape[1], D)
     h = F.silu(_lin(sincos, _w(sd, "t_embedder.1.linear_1.weight").float()))
     lora = _lin(h, _w(sd, "t_embedder.1.linear_2.weight").float())
+    if action is not None:
+        e_d, e_3d = action_embedding(cfg, sd, action)
+        sincos = sincos + e_d.float()
+        lora = lora + e_3d.float()
     emb_norm = te_rmsnorm(sincos, _w(sd, "t_embedding_norm.weight"))
     return emb_norm, lora
 
@@ -173,7 +198,7 @@ def block_forward(cfg, sd, i, x, emb, lora, ctx, freqs):
 
 def dit_forward(cfg: dict, sd: dict, x_B_C_T_H_W: torch.Tensor, timesteps_B_T: torch.Tensor,
                 crossattn_emb: torch.Tensor, cond_mask_B_1_T_H_W: torch.Tensor,
-                padding_mask_B_1_H_W: torch.Tensor | None = None) -> torch.Tensor:
+                padding_mask_B_1_H_W: torch.Tensor | None = None, action: torch.Tensor | None = None) -> torch.Tensor:
     """-> velocity [B, C, T, H, W] fp32 (the model applies .float(), text2world_model_rectified_flow.py:860)."""
     x = x_B_C_T_H_W.to(BF16)
     B, C, T, Hl, Wl = x.shape
@@ -195,7 +220,7 @@ def dit_forward(cfg: dict, sd: dict, x_B_C_T_H_W: torch.Tensor, timesteps_B_T: t
     if cfg["use_crossattn_projection"]:
         ctx = F.gelu(_lin(ctx, _w(sd, "crossattn_proj.0.weight"), _w(sd, "crossattn_proj.0.bias")))
 
-    emb, lora = timestep_embedding(cfg, sd, t)
+    emb, lora = timestep_embedding(cfg, sd, t, action)
     for i in range(cfg["num_blocks"]):
         x = block_forward(cfg, sd, i, x, emb, lora, ctx, freqs)
 

@@ -117,3 +117,33 @@ def test_sampler_matches_oracle(device, guidance, tol):
     err = _sampler_case(device, guidance)
     print(f"sampler vs oracle (Karras 2 steps = 3 evals x CFG, g={guidance}) rel-L2: {err:.3e}")
     assert err <= tol, err
+
+
+@pytest.mark.parametrize("per_frame", [4, 0])
+def test_action_dit_forward_matches_oracle(device, per_frame):
+    """Action-conditioned nets (action_conditioned_minimal_v1_lvg_dit.py): ActionChunk (4 actions per
+    latent frame, zero embedding for frame 0) and the per-chunk variant; same tolerance as the
+    plain forward (the action MLPs are bf16 torch ops on both sides)."""
+    cfg = tiny_dit(num_blocks=2, action_dim=7, action_per_latent_frame=per_frame, num_action_per_chunk=12)
+    sd, sd_ref = _setup(cfg, seed=2)
+    g = torch.Generator().manual_seed(12)
+    T, H, W = 4, 16, 16
+    x = torch.randn(1, 16, T, H, W, generator=g)
+    mask = torch.zeros(1, 1, T, H, W)
+    mask[:, :, :1] = 1
+    t = torch.tensor([[877.0] * T])
+    ctx = torch.randn(1, 512, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
+    action = (torch.randn(1, 12, 7, generator=g) * 2).to(torch.bfloat16)
+    ref = odit.dit_forward(dataclasses.asdict(cfg), sd_ref, x, t, ctx, mask, action=action)
+    ref0 = odit.dit_forward(dataclasses.asdict(cfg), sd_ref, x, t, ctx, mask, action=action * 0)
+    assert rel_l2(ref, ref0) > 1e-3  # the action changes the output
+    net = MinimalV1LVGDiT(cfg, device=device)
+    net.load_state_dict(sd_ref)
+    out = net(x.to(device).to(torch.bfloat16), t.to(device), ctx.to(device),
+              condition_video_input_mask_B_C_T_H_W=mask.to(device), action=action.to(device))
+    err = rel_l2(out.cpu(), ref)
+    print(f"action dit forward (per_latent_frame={per_frame}) rel-L2: {err:.3e}")
+    assert err <= 1e-2, err
+    with pytest.raises(ValueError):
+        net(x.to(device).to(torch.bfloat16), t.to(device), ctx.to(device),
+            condition_video_input_mask_B_C_T_H_W=mask.to(device))
