@@ -69,6 +69,8 @@ def state_dict_shapes(cfg: DiTConfig) -> Dict[str, Tuple[Tuple[int, ...], torch.
         for m in ("self_attn", "cross_attn", "mlp"):
             s[p + f"adaln_modulation_{m}.1.weight"] = ((A, D), BF16)
             s[p + f"adaln_modulation_{m}.2.weight"] = ((3 * D, A), BF16)
+    if cfg.n_cameras_emb:
+        s["view_embeddings.weight"] = ((cfg.n_cameras_emb, cfg.view_condition_dim), BF16)
     if cfg.action_dim:
         fin, hid = cfg.action_in_features, cfg.action_hidden_features
         for name, out in (("action_embedder_B_D", D), ("action_embedder_B_3D", 3 * D)):
@@ -102,6 +104,8 @@ def init_state_dict(cfg: DiTConfig, seed: int = 0, device="cpu", zero_adaln_out:
         elif name.startswith("pos_embedder.dim_"):
             full = 2 * shape[0] if "spatial" in name else 2 * shape[0]
             out[name] = (torch.arange(0, full, 2, device=device)[: shape[0]].float() / full).to(BF16)
+        elif name == "view_embeddings.weight":  # multiview_dit.py:390-391
+            out[name] = (torch.randn(shape, generator=g, device=device) * 0.02).to(BF16)
         elif name.startswith("action_embedder"):  # nn.Linear default init (not covered by init_weights)
             fan_in = shapes_fan[name]
             bound = 1.0 / math.sqrt(fan_in)
@@ -156,6 +160,15 @@ class Geometry:
     Wp: int  # patches along w
     tok0: int = 0  # first global token of this rank's shard
     n_tok: int = 0  # tokens on this rank
+    n_views: int = 1  # multi-view: T = n_views x per-view frames, tokens ordered (view, t, h, w)
+
+    @property
+    def T_view(self) -> int:
+        return self.T // self.n_views
+
+    @property
+    def L_view(self) -> int:
+        return self.L // self.n_views
 
     @property
     def hw(self) -> int:
@@ -257,9 +270,12 @@ class MinimalV1LVGDiT:
         return ContextCache(B=B, k=ks, v=vs)
 
     def rope_tables(self, geo: Geometry) -> Tuple[torch.Tensor, torch.Tensor]:
-        key = (geo.T, geo.Hp, geo.Wp)
+        """cos/sin [n_tok, 64] of this shard; multi-view: every view's positions restart at t = 0
+        (MultiCameraVideoRopePosition3DEmb.generate_embeddings, multiview_dit.py:108-130)."""
+        key = (geo.T, geo.Hp, geo.Wp, geo.n_views)
         if key not in self._rope_cache:
-            fr = rope_freqs(self.cfg, geo.T, geo.Hp, geo.Wp, self.sd, self.device)[:, :64].contiguous()
+            fr = rope_freqs(self.cfg, geo.T_view, geo.Hp, geo.Wp, self.sd, self.device)[:, :64]
+            fr = fr.repeat(geo.n_views, 1).contiguous()
             self._rope_cache[key] = (torch.cos(fr).contiguous(), torch.sin(fr).contiguous())
         c, s = self._rope_cache[key]
         return c[geo.tok0: geo.tok0 + geo.n_tok], s[geo.tok0: geo.tok0 + geo.n_tok]
@@ -339,8 +355,43 @@ class MinimalV1LVGDiT:
 
     # ---------------------------------------------------------------- hot path
     @torch.no_grad()
+    def n_views_for(self, T: int) -> int:
+        """Views stacked along the latent T axis (multi-view nets: T / state_t, MultiViewDiT :461)."""
+        cfg = self.cfg
+        if not cfg.n_cameras_emb:
+            return 1
+        if cfg.state_t <= 0 or T % cfg.state_t:
+            raise ValueError(f"{T} latent frames are not a whole number of {cfg.state_t}-frame views")
+        return T // cfg.state_t
+
+    def embed_patches(self, patch_rows: torch.Tensor, geo: Geometry,
+                      view_indices: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """x_embedder (PatchEmbed Linear, minimal_v4_dit.py:846-913) of [n, Bx, 72] patch rows -> [n, Bx, D].
+        Multi-view nets also concatenate a view embedding as input channels
+        (prepare_embedded_sequence, multiview_dit.py:462-490); those channels are constant over a view, so
+        their patch features (c, p1, p2) fold into one per-view bias: y = rows W72^T + e_v Wv^T, summed
+        in fp32 and rounded once to bf16 like the reference's single bf16 GEMM."""
+        cfg = self.cfg
+        p = self.sd
+        D = cfg.model_channels
+        n, Bx, f = patch_rows.shape
+        w = p["x_embedder.proj.1.weight"]
+        if not cfg.view_condition_dim:
+            return F.linear(patch_rows.reshape(n * Bx, f), w).view(n, Bx, D)
+        V = geo.n_views
+        if view_indices is None:
+            view_indices = torch.arange(V, device=self.device)
+        view_indices = view_indices.to(self.device).long().clamp(max=cfg.n_cameras_emb - 1)
+        emb = p["view_embeddings.weight"][view_indices].float()  # [V, vdim]
+        wv = w[:, f:].float().view(D, cfg.view_condition_dim, -1).sum(-1)  # [D, vdim]
+        bias = emb @ wv.t()  # [V, D]
+        view_of_tok = torch.arange(geo.tok0, geo.tok0 + n, device=self.device) // geo.L_view
+        y = F.linear(patch_rows.reshape(n * Bx, f).float(), w[:, :f].float()).view(n, Bx, D)
+        return (y + bias[view_of_tok][:, None, :]).to(BF16)
+
     def forward_tokens(self, patch_rows: torch.Tensor, t_B_T: torch.Tensor, ctx: ContextCache,
-                       geo: Geometry, action: Optional[torch.Tensor] = None) -> torch.Tensor:
+                       geo: Geometry, action: Optional[torch.Tensor] = None,
+                       view_indices: Optional[torch.Tensor] = None) -> torch.Tensor:
         """patch_rows: [n_tok, Bx, 72] bf16 (Bx = 1 shares the input across the CFG batch);
         t_B_T: [B, T] fp32, already scaled. Returns the final layer output [n_tok, B, 64] fp32
         (feature order (p1 p2 C) = patch layout).
@@ -358,7 +409,7 @@ class MinimalV1LVGDiT:
         D = cfg.model_channels
         n = geo.n_tok
         Bx = patch_rows.shape[1]
-        x_in = F.linear(patch_rows.reshape(n * Bx, -1), p["x_embedder.proj.1.weight"]).view(n, Bx, D)
+        x_in = self.embed_patches(patch_rows, geo, view_indices)
         mods, shift_f, scale_f = self.time_modulation(t_B_T, action)
         cos, sin = self.rope_tables(geo)
         cp = self.cp_group
@@ -454,8 +505,7 @@ class MinimalV1LVGDiT:
             qc = F.linear(h.view(n * B, D), p[pre + "cross_attn.q_proj.weight"])
             N.head_rmsnorm_rope(qc, n_rows=n * B, B=B, H=H, head_off=0, weight=p[pre + "cross_attn.q_norm.weight"])
             o = torch.empty((n, B, D), dtype=BF16, device=self.device)
-            N.attn_fwd(qc.view(n, B, H, hd).transpose(0, 1), ctx.k[i], ctx.v[i],
-                       out=o.view(n, B, H, hd).transpose(0, 1), softmax_scale=scale_attn)
+            self._cross_attention(qc.view(n, B, H, hd), ctx.k[i], ctx.v[i], o.view(n, B, H, hd), geo, scale_attn)
             y = F.linear(o.view(n * B, D), p[pre + "cross_attn.output_proj.weight"])
             _, _, g_ca = mod(i, 1)
             sh, sc, _ = mod(i, 2)
@@ -479,6 +529,26 @@ class MinimalV1LVGDiT:
         xf = N.final_ln_mod(x, shift_f, scale_f, y=y, gate=gate_prev, **common)
         out = F.linear(xf.view(n * B, D), self.w_final)
         return out.view(n, B, -1)
+
+    def _cross_attention(self, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, o: torch.Tensor, geo: Geometry,
+                         scale: float) -> None:
+        """Text cross-attention of this shard's queries q/o [n, B, H, hd] against k/v [B, Lc, H, hd].
+        Multi-view context holds 512 tokens per view and each view's queries see only their own
+        (MultiViewCrossAttention, multiview_dit.py:40-55); a shard may span view boundaries."""
+        n = q.shape[0]
+        n_ctx = k.shape[1] // 512 if k.shape[1] % 512 == 0 else 1
+        if geo.n_views == 1 or n_ctx == 1:
+            N.attn_fwd(q.transpose(0, 1), k, v, out=o.transpose(0, 1), softmax_scale=scale)
+            return
+        if n_ctx != geo.n_views:
+            raise ValueError(f"context has {n_ctx} x 512 tokens for {geo.n_views} views")
+        for vi in range(geo.n_views):
+            a = max(geo.tok0, vi * geo.L_view) - geo.tok0
+            b = min(geo.tok0 + n, (vi + 1) * geo.L_view) - geo.tok0
+            if a >= b:
+                continue
+            ks = slice(vi * 512, (vi + 1) * 512)
+            N.attn_fwd(q[a:b].transpose(0, 1), k[:, ks], v[:, ks], out=o[a:b].transpose(0, 1), softmax_scale=scale)
 
     def _cp_self_attention(self, i: int, h: torch.Tensor, o: torch.Tensor, cos, sin, n: int, B: int, cp,
                            cp_size: int, e0=None):
@@ -519,7 +589,11 @@ class MinimalV1LVGDiT:
         cfg = self.cfg
         B, C, T, Hl, Wl = x_B_C_T_H_W.shape
         Hp, Wp = Hl // cfg.patch_spatial, Wl // cfg.patch_spatial
-        geo = Geometry(T=T, Hp=Hp, Wp=Wp, tok0=0, n_tok=T * Hp * Wp)
+        geo = Geometry(T=T, Hp=Hp, Wp=Wp, tok0=0, n_tok=T * Hp * Wp, n_views=self.n_views_for(T))
+        view_indices = None
+        vi_bt = kwargs.get("view_indices_B_T")
+        if vi_bt is not None and cfg.n_cameras_emb:  # [B, V*T] -> one index per view (multiview_dit.py:474-478)
+            view_indices = vi_bt[0, ::geo.T_view]
         x = x_B_C_T_H_W.to(self.device, BF16)
         if condition_video_input_mask_B_C_T_H_W is None:
             mask = torch.zeros(B, 1, T, Hl, Wl, dtype=BF16, device=self.device)
@@ -539,7 +613,8 @@ class MinimalV1LVGDiT:
         t = timesteps_B_T.to(self.device).float() * cfg.timestep_scale
         if t.shape[1] == 1 and T > 1:
             t = t.expand(B, T).contiguous()
-        out = self.forward_tokens(rows.contiguous(), t, ctx, geo, action=action)  # [L, B, 64] (p1 p2 C)
+        out = self.forward_tokens(rows.contiguous(), t, ctx, geo, action=action,
+                                  view_indices=view_indices)  # [L, B, 64] (p1 p2 C)
         out = out.view(T, Hp, Wp, B, 2, 2, C).permute(3, 6, 0, 1, 4, 2, 5)
         return out.reshape(B, C, T, Hl, Wl).float()
 

@@ -100,13 +100,14 @@ class Video2WorldModelRectifiedFlow:
     def sample_latents(self, gt: Optional[torch.Tensor], ctx_cond: torch.Tensor, ctx_uncond: torch.Tensor, *,
                        state_shape, num_conditional_frames: int, guidance: float, seed: int, num_steps: int,
                        shift: float = 5.0, cfg_mode: Optional[str] = None, progress=None,
-                       net_fn=None, action: Optional[torch.Tensor] = None) -> torch.Tensor:
+                       net_fn=None, action: Optional[torch.Tensor] = None,
+                       view_indices: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Core loop. gt: x0 latent [1, C, T, H, W] fp32 (or None when no frame is conditioned);
         ctx_*: text embeddings [1, Lctx, proj_in]. Returns latents [1, C, T, H, W] fp32.
         net_fn(rows [n,1,72] bf16, t_B_T [2,T] fp32, geo) -> [n,2,64] replaces the DiT (tests only)."""
         C, T, H, W = state_shape
         dev = self.device
-        geo = Geometry(T=T, Hp=H // 2, Wp=W // 2)
+        geo = Geometry(T=T, Hp=H // 2, Wp=W // 2, n_views=self.net.n_views_for(T))
         L = geo.L
         cp = self.cp_group
         rank, world = (0, 1) if cp is None else (torch.distributed.get_rank(cp), torch.distributed.get_world_size(cp))
@@ -120,8 +121,11 @@ class Video2WorldModelRectifiedFlow:
         noise = to_patch_layout(noise_full[0])[sl].contiguous()
         del noise_full
         frame_mask = torch.zeros(T, dtype=torch.float32, device=dev)
-        if T > 1 and num_conditional_frames > 0:
-            frame_mask[:num_conditional_frames] = 1.0
+        if geo.T_view > 1 and num_conditional_frames > 0:
+            # the first frames of every view (multi-view FIRST_RANDOM_N, predict2_multiview/configs/vid2vid/
+            # defaults/conditioner.py:125-260; one view: video2world conditioner.py:45-143)
+            for vi in range(geo.n_views):
+                frame_mask[vi * geo.T_view: vi * geo.T_view + num_conditional_frames] = 1.0
         gtp = None
         if gt is not None and num_conditional_frames > 0:
             gtp = to_patch_layout(gt[0].to(dev, torch.float32))[sl].contiguous()
@@ -139,7 +143,8 @@ class Video2WorldModelRectifiedFlow:
             tf = self._frame_timesteps(t, frame_mask)  # [T]
             t_B_T = (tf[None, :] * scale).expand(2, T).contiguous()
             if net_fn is None:
-                net_out = self.net.forward_tokens(rows.view(geo.n_tok, 1, -1), t_B_T, ctx, geo, action=action)
+                net_out = self.net.forward_tokens(rows.view(geo.n_tok, 1, -1), t_B_T, ctx, geo, action=action,
+                                                  view_indices=view_indices)
             else:
                 net_out = net_fn(rows.view(geo.n_tok, 1, -1), t_B_T, geo)
             v = N.cfg_velocity(net_out, noise, gtp, frame_mask, guidance, mode, tok0=geo.tok0, hw=geo.hw)

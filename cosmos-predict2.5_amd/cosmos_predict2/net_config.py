@@ -49,6 +49,14 @@ class DiTConfig:
     action_per_latent_frame: int = 0
     num_action_per_chunk: int = 12
     action_hidden: int = 0  # hidden width of the embedder MLPs (0 = 4 * model_channels)
+    # multi-view (cosmos_predict2/_src/predict2_multiview/networks/multiview_dit.py:268-325): n_cameras_emb > 0
+    # adds view_embeddings (nn.Embedding(n_cameras_emb, view_condition_dim)) concatenated to the input
+    # channels of every view (concat_view_embedding); views are stacked along T (state_t latent frames
+    # each), self-attention runs over all views jointly, RoPE positions restart per view
+    # (MultiCameraVideoRopePosition3DEmb :103-130), cross-attention is per view (512 text tokens each, :40-55)
+    n_cameras_emb: int = 0
+    view_condition_dim: int = 0
+    state_t: int = 0
 
     @property
     def head_dim(self) -> int:
@@ -57,7 +65,8 @@ class DiTConfig:
     @property
     def patch_features(self) -> int:
         # (in_channels + cond mask + padding mask) * p_t * p_s * p_s
-        return (self.in_channels + 1 + int(self.concat_padding_mask)) * self.patch_temporal * self.patch_spatial ** 2
+        return ((self.in_channels + 1 + int(self.concat_padding_mask) + self.view_condition_dim)
+                * self.patch_temporal * self.patch_spatial ** 2)
 
     @property
     def mlp_hidden(self) -> int:
@@ -102,6 +111,14 @@ SAMPLER_PRE_TRAINED = SamplerConfig()
 # (:308-320) apply on top of the /net group default.
 DIT_2B_ACTION = DIT_2B.replace(action_dim=7, action_per_latent_frame=4)
 SAMPLER_ACTION = SamplerConfig(state_t=4, resolution="256")
+# auto/multiview (checkpoint_db.py:397-415, experiment buttercup_predict2p5_2b_7views_res720p_fps30_t8_..._nofps,
+# predict2_multiview/configs/vid2vid/experiment/buttercup/buttercup2p5_rectified_flow.py:30-75, 529-550;
+# net COSMOS_V1_2B_MULTIVIEW_NET, defaults/net.py:26-63): 7 camera embeddings of 7 channels, state_t 8 per
+# view (29 frames), RoPE h/w 3.0, t 8/24, fps modulation off; CFG uncond + g (cond - uncond)
+# (multiview_vid2vid_model_rectified_flow.py:381); the first n latent frames of every view are conditioned.
+DIT_2B_MULTIVIEW = DIT_2B.replace(n_cameras_emb=7, view_condition_dim=7, state_t=8,
+                                  rope_t_extrapolation_ratio=8.0 / 24.0)
+SAMPLER_MULTIVIEW = SamplerConfig(state_t=8, cfg_mode="text2world", resolution="720")
 
 # model name (cosmos_predict2/config.py ModelKey.name) -> (net, sampler)
 MODELS = {
@@ -109,6 +126,7 @@ MODELS = {
     "2B/pre-trained": (DIT_2B, SAMPLER_PRE_TRAINED),
     "14B/pre-trained": (DIT_14B, SAMPLER_PRE_TRAINED),
     "2B/robot/action-cond": (DIT_2B_ACTION, SAMPLER_ACTION),
+    "2B/auto/multiview": (DIT_2B_MULTIVIEW, SAMPLER_MULTIVIEW),
 }
 
 # Subset of VIDEO_RES_SIZE_INFO (cosmos_predict2/_src/predict2/datasets/utils.py:44-67); the model's

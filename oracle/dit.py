@@ -152,8 +152,8 @@ def ln_mod(x, shift, scale):
     return F.layer_norm(x, (x.shape[-1],), eps=1e-6) * (1 + scale) + shift
 
 
-def block_forward(cfg, sd, i, x, emb, lora, ctx, freqs):
-    """Block.forward, x [B, T, H, W, D] bf16."""
+def block_forward(cfg, sd, i, x, emb, lora, ctx, freqs, n_views: int = 1):
+    """Block.forward, x [B, T, H, W, D] bf16 (multi-view: MultiViewBlock, per-view cross-attention)."""
     p = f"blocks.{i}."
     nh, hd = cfg["num_heads"], cfg["model_channels"] // cfg["num_heads"]
     sh_sa, sc_sa, g_sa = adaln(sd, p + "adaln_modulation_self_attn", emb, lora)
@@ -185,7 +185,16 @@ def block_forward(cfg, sd, i, x, emb, lora, ctx, freqs):
     v = _lin(ctx, _w(sd, p + "cross_attn.v_proj.weight")).reshape(B, -1, nh, hd)
     q = te_rmsnorm(q, _w(sd, p + "cross_attn.q_norm.weight"))
     k = te_rmsnorm(k, _w(sd, p + "cross_attn.k_norm.weight"))
-    o = sdpa(q, k, v)
+    nv = ctx.shape[1] // 512
+    if n_views > 1 and nv > 1:
+        # MultiViewCrossAttention (multiview_dit.py:46-55): B (V L) D -> (V B) L D, context B (V M) D -> (V B) M D
+        Lq = q.shape[1] // nv
+        q = q.view(B, nv, Lq, nh, hd).transpose(0, 1).reshape(nv * B, Lq, nh, hd)
+        k = k.view(B, nv, 512, nh, hd).transpose(0, 1).reshape(nv * B, 512, nh, hd)
+        v = v.view(B, nv, 512, nh, hd).transpose(0, 1).reshape(nv * B, 512, nh, hd)
+        o = sdpa(q, k, v).view(nv, B, Lq, nh * hd).transpose(0, 1).reshape(B, nv * Lq, nh * hd)
+    else:
+        o = sdpa(q, k, v)
     o = _lin(o, _w(sd, p + "cross_attn.output_proj.weight")).reshape(B, T, H, W, D)
     x = o * g_ca + x
 
@@ -208,13 +217,22 @@ def dit_forward(cfg: dict, sd: dict, x_B_C_T_H_W: torch.Tensor, timesteps_B_T: t
         pm = padding_mask_B_1_H_W if padding_mask_B_1_H_W is not None else torch.zeros(B, 1, Hl, Wl)
         pm = F.interpolate(pm.float(), size=(Hl, Wl), mode="nearest").to(BF16)
         x = torch.cat([x, pm[:, :, None].expand(B, 1, T, Hl, Wl)], dim=1)
+    n_views = T // cfg["state_t"] if cfg.get("n_cameras_emb", 0) else 1
+    if n_views > 1 or cfg.get("n_cameras_emb", 0):
+        # concat_view_embedding (multiview_dit.py:462-490): view channels after [x, mask, padding mask]
+        vidx = torch.arange(n_views).clamp(max=cfg["n_cameras_emb"] - 1)
+        ve = _w(sd, "view_embeddings.weight")[vidx]  # [V, vdim] bf16
+        Tv = T // n_views
+        vch = ve.t()[None, :, :, None, None, None].expand(B, ve.shape[1], n_views, Tv, Hl, Wl)
+        x = torch.cat([x.view(B, x.shape[1], n_views, Tv, Hl, Wl), vch.to(BF16)], 1).reshape(B, -1, T, Hl, Wl)
     ps, pt = cfg["patch_spatial"], cfg["patch_temporal"]
     Tp, Hp, Wp = T // pt, Hl // ps, Wl // ps
     # b c (t r) (h m) (w n) -> b t h w (c r m n)
     xp = x.reshape(B, x.shape[1], Tp, pt, Hp, ps, Wp, ps).permute(0, 2, 4, 6, 1, 3, 5, 7)
     xp = xp.reshape(B, Tp, Hp, Wp, -1)
     x = _lin(xp, _w(sd, "x_embedder.proj.1.weight"))
-    freqs = rope_freqs(cfg, Tp, Hp, Wp)
+    # MultiCameraVideoRopePosition3DEmb (multiview_dit.py:108-130): positions restart per view
+    freqs = rope_freqs(cfg, Tp // n_views, Hp, Wp).repeat(n_views, 1)
 
     ctx = crossattn_emb.to(BF16)
     if cfg["use_crossattn_projection"]:
@@ -222,7 +240,7 @@ def dit_forward(cfg: dict, sd: dict, x_B_C_T_H_W: torch.Tensor, timesteps_B_T: t
 
     emb, lora = timestep_embedding(cfg, sd, t, action)
     for i in range(cfg["num_blocks"]):
-        x = block_forward(cfg, sd, i, x, emb, lora, ctx, freqs)
+        x = block_forward(cfg, sd, i, x, emb, lora, ctx, freqs, n_views)
 
     # final layer (fp32 autocast)
     D = cfg["model_channels"]

@@ -42,3 +42,14 @@ def test_action_model_registered():
     with pytest.raises(NotImplementedError):
         get_action_sequence_from_states({"state": np.zeros((3, 6)), "continuous_gripper_state": np.zeros(3)},
                                         use_quat=True)
+
+
+def test_multiview_model_registered():
+    net, samp = MODELS["2B/auto/multiview"]
+    assert net.n_cameras_emb == 7 and net.view_condition_dim == 7 and net.state_t == 8
+    assert net.patch_features == (16 + 1 + 1 + 7) * 4  # x_embedder [2048, 100]
+    assert samp.cfg_mode == "text2world"
+    from cosmos_predict2.dit import state_dict_shapes
+
+    s = state_dict_shapes(net)
+    assert s["x_embedder.proj.1.weight"][0] == (2048, 100) and s["view_embeddings.weight"][0] == (7, 7)
