@@ -177,3 +177,24 @@ def test_multiview_dit_forward_matches_oracle(device):
     out2 = net(x.to(device).to(torch.bfloat16), t.to(device), ctx.to(device),
                condition_video_input_mask_B_C_T_H_W=mask.to(device))
     assert rel_l2(out2.cpu(), out.cpu()) > 1e-3
+
+
+def test_14b_width_block_matches_oracle(device):
+    """14B layout (model_channels 5120, 40 heads of 128: net.py COSMOS_V1_14B_NET_MININET) through one
+    block: every kernel at D = 5120 (LN-mod, RMSNorm+RoPE, attention over 40 heads)."""
+    cfg = tiny_dit(model_channels=5120, num_heads=40, num_blocks=1, adaln_lora_dim=256)
+    sd, sd_ref = _setup(cfg, seed=5)
+    g = torch.Generator().manual_seed(15)
+    T, H, W = 2, 16, 16
+    x = torch.randn(1, 16, T, H, W, generator=g)
+    mask = torch.zeros(1, 1, T, H, W)
+    t = torch.tensor([[500.0, 500.0]])
+    ctx = torch.randn(1, 512, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
+    ref = odit.dit_forward(dataclasses.asdict(cfg), sd_ref, x, t, ctx, mask)
+    net = MinimalV1LVGDiT(cfg, device=device)
+    net.load_state_dict(sd_ref)
+    out = net(x.to(device).to(torch.bfloat16), t.to(device), ctx.to(device),
+              condition_video_input_mask_B_C_T_H_W=mask.to(device))
+    err = rel_l2(out.cpu(), ref)
+    print(f"14B-width block rel-L2: {err:.3e}")
+    assert err <= 1e-2, err
