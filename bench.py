@@ -42,6 +42,9 @@ def parse():
     ap.add_argument("--resolution", default="704,1280")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--backend", default="nccl", help="process-group backend for N > 1 (nccl = RCCL; gloo only "
+                    "for rehearsing the multi-rank flow with several ranks on one GPU, see --share-device)")
+    ap.add_argument("--share-device", action="store_true", help="every rank uses cuda:0 (rehearsal on one GPU)")
     return ap.parse_args()
 
 
@@ -65,10 +68,13 @@ def main():
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}: launch N>1 with torch.distributed.run")
     _heartbeat(rank)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", 0 if a.share_device else local)
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(a.backend)
 
     from cosmos_predict2.pipeline import Video2WorldInference
     from cosmos_predict2 import _native
