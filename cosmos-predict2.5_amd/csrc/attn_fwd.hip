@@ -85,7 +85,7 @@ struct AttnArgs {
   float* lse_part;  // nsplit > 1: [nsplit][B][H][Lq] fp32 log2-sum-exp2 of the scaled scores
   float scale_log2; // softmax scale * log2(e)
 #ifdef CP25_ATTN_PROBE
-  unsigned long long* probe;  // [wg < 8][wave][tile - probe_t0 < 32][4] s_memtime stamps (lab build only)
+  unsigned long long* probe;  // [wg < 8][wave][tile - probe_t0 < 32][8] s_memtime stamps (lab build only)
   int probe_t0;
 #endif
 };
@@ -97,7 +97,7 @@ struct AttnArgs {
   do {                                                                                                \
     const int pt_ = (t) - a.probe_t0;                                                                 \
     if (a.probe && blockIdx.x < 8 && pt_ >= 0 && pt_ < 32)                                                 \
-      a.probe[(((size_t)blockIdx.x * kWaves + wave) * 32 + pt_) * 4 + (k)] = __builtin_amdgcn_s_memtime(); \
+      a.probe[(((size_t)blockIdx.x * kWaves + wave) * 32 + pt_) * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
 #define ATTN_STAMP(t, k) do { } while (0)
@@ -342,7 +342,9 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
       ATTN_STAMP(t, 1);
       if (t + 1 < ntiles) {
         softmax(t + 1);
+        ATTN_STAMP(t, 4);
         write_v(std::integral_constant<int, par ^ 1>{});
+        ATTN_STAMP(t, 5);
         load_tile(t + 2);
       }
       ATTN_STAMP(t, 2);
@@ -358,8 +360,10 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
     // group B: phase 2t softmax(t) + K(t+2) staging, phase 2t+1 MFMA
     auto step = [&](auto PAR, int t) __attribute__((always_inline)) {
       softmax(t);
+      ATTN_STAMP(t, 4);
       if (t + 2 < ntiles) {
         write_k(PAR);
+        ATTN_STAMP(t, 5);
         load_tile(t + 3);
       }
       ATTN_STAMP(t, 0);

@@ -34,7 +34,7 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     q, k, v = (torch.randn(a.B, a.L, a.H, 128, device=dev, generator=g).to(torch.bfloat16) for _ in range(3))
     o = torch.empty_like(q)
-    probe = torch.zeros(8 * 8 * 32 * 4, dtype=torch.int64, device=dev)
+    probe = torch.zeros(8 * 8 * 32 * 8, dtype=torch.int64, device=dev)
 
     def strides(t):
         return (ctypes.c_int64 * 3)(t.stride(0), t.stride(1), t.stride(2))
@@ -59,7 +59,7 @@ def main():
     lib.cp25_attn_probe_set(ctypes.c_void_p(probe.data_ptr()), a.t0)
     run()
     torch.cuda.synchronize()
-    T = probe.cpu().numpy().astype(np.int64).reshape(8, 8, 32, 4)  # wg, wave, tile, stamp
+    T = probe.cpu().numpy().astype(np.int64).reshape(8, 8, 32, 8)  # wg, wave, tile, stamp
     res = {"L": a.L, "ms": ms, "tflops": 4 * a.B * a.H * a.L * a.L * 128 / ms / 1e9}
     for name, waves in (("A", range(0, 4)), ("B", range(4, 8))):
         t = T[:, list(waves)]
@@ -70,8 +70,14 @@ def main():
             "ph2": (t[..., 2] - t[..., 1]).mean(),
             "bar2": (t[..., 3] - t[..., 2]).mean(),
         }
+        # softmax-phase split: softmax VALU | wait for the staged loads + LDS write | load issue
+        sm_start = t[:, :, 1:, 1] if name == "A" else t[:, :, 1:, 3 - 3] * 0 + np.concatenate(
+            [t[:, :, :1, 3] * 0, t[:, :, :-1, 3]], axis=2)[:, :, 1:]
+        d["softmax_valu"] = (t[:, :, 1:, 4] - sm_start).mean()
+        d["stage_wait_write"] = (t[:, :, 1:, 5] - t[:, :, 1:, 4]).mean()
         res[name] = {k: round(float(x), 1) for k, x in d.items()}
-    res["note"] = "A: ph1 = MFMA phase, ph2 = softmax; B: ph1 = softmax, ph2 = MFMA (cycles of s_memtime)"
+    res["note"] = ("A: ph1 = MFMA phase, ph2 = softmax; B: ph1 = softmax, ph2 = MFMA (cycles of s_memtime); "
+                   "softmax_valu / stage_wait_write split the softmax phase")
     print(json.dumps(res))
 
 

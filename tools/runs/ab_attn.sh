@@ -1,7 +1,7 @@
 set -o pipefail
 export PYTHONUNBUFFERED=1
 for r in 1 2 3; do
-  for v in base sum2 priob both; do
+  for v in base st32 st16; do
     timeout -k 10 60 python tools/bench_attn.py --L 109120 --iters 3 --lib tools/lab/libcp25_$v.so >> gpurun_out/ab_attn.log 2>&1 || exit 1
   done
 done
