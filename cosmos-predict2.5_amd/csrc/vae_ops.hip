@@ -66,8 +66,26 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
   const int kc_per_tap = a.Cin / BK;
   const int nk = a.KT * a.KH * a.KW * kc_per_tap;
 
-  // per-thread A rows (pixels) this thread stages
+  // per-thread A rows (pixels) this thread stages: their output coordinates are fixed for the whole
+  // K loop, so the pixel -> (ho, wo) division and the padding offsets are done once here; a k-step
+  // only adds its tap (kh, kw)
   u32x4 ra[A_PER_T], rb[B_PER_T];
+  int a_h0[A_PER_T], a_w0[A_PER_T], a_off[A_PER_T];
+#pragma unroll
+  for (int i = 0; i < A_PER_T; ++i) {
+    const int c = tid + 256 * i;
+    const int row = c / CPR, ch = c % CPR;
+    const int p = m0 + row;
+    a_off[i] = ch * 8;
+    if (c < A_CHUNKS && p < M) {
+      const int ho = p / a.Wo, wo = p % a.Wo;
+      a_h0[i] = a.upsample ? ho - a.pad_top : ho * a.stride_hw - a.pad_top;
+      a_w0[i] = a.upsample ? wo - a.pad_left : wo * a.stride_hw - a.pad_left;
+    } else {
+      a_h0[i] = -(1 << 28);  // never in range
+      a_w0[i] = 0;
+    }
+  }
 
   auto load_stage = [&](int ks) {
     const int tap = ks / kc_per_tap;
@@ -79,27 +97,21 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
     const unsigned short* fr = (fi < a.n_frames) ? a.frames[fi] : nullptr;
 #pragma unroll
     for (int i = 0; i < A_PER_T; ++i) {
-      const int c = tid + 256 * i;
       u32x4 v = {0u, 0u, 0u, 0u};
-      if (c < A_CHUNKS) {
-        const int row = c / CPR, ch = c % CPR;
-        const int p = m0 + row;
-        if (fr != nullptr && p < M) {
-          const int ho = p / a.Wo, wo = p % a.Wo;
-          int hi, wi;
-          bool ok;
-          if (a.upsample) {
-            const int hu = ho + kh - a.pad_top, wu = wo + kw - a.pad_left;
-            ok = hu >= 0 && hu < 2 * a.Hin && wu >= 0 && wu < 2 * a.Win;
-            hi = hu >> 1;
-            wi = wu >> 1;
-          } else {
-            hi = ho * a.stride_hw + kh - a.pad_top;
-            wi = wo * a.stride_hw + kw - a.pad_left;
-            ok = hi >= 0 && hi < a.Hin && wi >= 0 && wi < a.Win;
-          }
-          if (ok) v = *reinterpret_cast<const u32x4*>(fr + ((int64_t)hi * a.Win + wi) * a.Cin + c0 + ch * 8);
+      if (fr != nullptr) {
+        int hi, wi;
+        bool ok;
+        if (a.upsample) {
+          const int hu = a_h0[i] + kh, wu = a_w0[i] + kw;
+          ok = hu >= 0 && hu < 2 * a.Hin && wu >= 0 && wu < 2 * a.Win;
+          hi = hu >> 1;
+          wi = wu >> 1;
+        } else {
+          hi = a_h0[i] + kh;
+          wi = a_w0[i] + kw;
+          ok = hi >= 0 && hi < a.Hin && wi >= 0 && wi < a.Win;
         }
+        if (ok) v = *reinterpret_cast<const u32x4*>(fr + ((int64_t)hi * a.Win + wi) * a.Cin + c0 + a_off[i]);
       }
       ra[i] = v;
     }
