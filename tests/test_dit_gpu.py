@@ -198,3 +198,29 @@ def test_14b_width_block_matches_oracle(device):
     err = rel_l2(out.cpu(), ref)
     print(f"14B-width block rel-L2: {err:.3e}")
     assert err <= 1e-2, err
+
+
+def test_config1_shape_2b_width_sampler_matches_oracle(device):
+    """BASELINE config 1 geometry (256x256x9 frames -> latent [16, 3, 32, 32], 768 tokens; Karras
+    2 steps = 3 evals x CFG; conditional frame t 0.1) at the real 2B widths (D 2048, 16 heads,
+    crossattn_proj 100352 -> 1024, AdaLN-LoRA 256), two of the 28 blocks so the CPU oracle finishes in
+    seconds; guidance 0 (see test_sampler_matches_oracle for the guidance amplification)."""
+    from cosmos_predict2.net_config import DIT_2B
+
+    cfg = DIT_2B.replace(num_blocks=2)
+    sd, sd_ref = _setup(cfg, seed=7)
+    T, H, W = 3, 32, 32
+    g = torch.Generator().manual_seed(70)
+    gt = torch.randn(1, 16, T, H, W, generator=g)
+    ctx_c = torch.randn(1, 512, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
+    ctx_u = torch.randn(1, 512, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
+    model = Video2WorldModelRectifiedFlow(cfg, SamplerConfig(use_kerras_sigma_at_inference=True,
+                                                             conditional_frame_timestep=0.1), device=device)
+    model.load_state_dict(sd_ref)
+    kw = dict(num_cond=1, guidance=0.0, seed=0, num_steps=2, use_karras=True, cond_frame_t=0.1)
+    ref = osamp.generate(dataclasses.asdict(cfg), sd_ref, gt, ctx_c, ctx_u, **kw)
+    out = model.sample_latents(gt.to(device), ctx_c.to(device), ctx_u.to(device), state_shape=(16, T, H, W),
+                               num_conditional_frames=1, guidance=0.0, seed=0, num_steps=2)
+    err = rel_l2(out.cpu(), ref)
+    print(f"config-1 shape, 2B widths (2 blocks) sampler vs oracle rel-L2: {err:.3e}")
+    assert err <= 1e-2, err
