@@ -341,9 +341,10 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
       __syncthreads();
       ATTN_STAMP(t, 1);
       if (t + 1 < ntiles) {
-        softmax(t + 1);
-        ATTN_STAMP(t, 4);
+        // the staged V(t+1) goes to LDS before the softmax: its LDS write drains under the VALU
+        // (+0.7 % measured against writing after the softmax)
         write_v(std::integral_constant<int, par ^ 1>{});
+        softmax(t + 1);
         ATTN_STAMP(t, 5);
         load_tile(t + 2);
       }
@@ -359,13 +360,10 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   } else {
     // group B: phase 2t softmax(t) + K(t+2) staging, phase 2t+1 MFMA
     auto step = [&](auto PAR, int t) __attribute__((always_inline)) {
+      if (t + 2 < ntiles) write_k(PAR);  // LDS write first, drains under the softmax VALU
       softmax(t);
       ATTN_STAMP(t, 4);
-      if (t + 2 < ntiles) {
-        write_k(PAR);
-        ATTN_STAMP(t, 5);
-        load_tile(t + 3);
-      }
+      if (t + 2 < ntiles) load_tile(t + 3);
       ATTN_STAMP(t, 0);
       __syncthreads();
       ATTN_STAMP(t, 1);
