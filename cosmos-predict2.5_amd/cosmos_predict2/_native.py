@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from typing import Optional
+from typing import Optional, Tuple
 
 import torch
 
@@ -51,6 +51,8 @@ SIGNATURES = {
     "cp25_attn_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, c_int64_p, _F, _P],
     "cp25_attn_fwd_split": [_P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, c_int64_p, _F, _I,
                             _P, ctypes.c_size_t, _P],
+    "cp25_attn_fwd_bounded": [_P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, c_int64_p, _F, _F,
+                              _F, _I, _P, ctypes.c_size_t, _P],
     "cp25_attn_workspace_bytes": [_I, _I, _I, _I],
     "cp25_attn_plan": [_I, _I, _I, _I, _I],
     "cp25_ln_mod": [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _P, _P, _I64, _I, _I, _I64, _I64, _F, _P],
@@ -132,10 +134,13 @@ def attn_plan(B: int, H: int, Lq: int, Lk: int, D: int = 128) -> int:
 
 
 def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[torch.Tensor] = None,
-             softmax_scale: Optional[float] = None, n_split: Optional[int] = None) -> torch.Tensor:
+             softmax_scale: Optional[float] = None, n_split: Optional[int] = None,
+             norm_bounds: Optional[Tuple[float, float]] = None) -> torch.Tensor:
     """softmax(q k^T * scale) v for q [B, Lq, H, 128], k/v [B, Lk, H, 128] (bf16, any strides with
     a contiguous head dim). Returns [B, Lq, H, 128] bf16. n_split: key-range split (None = the
-    library's plan for this shape; the fp32 partials live in a caching-allocator workspace)."""
+    library's plan for this shape; the fp32 partials live in a caching-allocator workspace).
+    norm_bounds: (max |q|, max |k|) upper bounds over all rows, enabling the bounded-shift softmax
+    where they are small enough (cp25_attn_fwd_bounded; None = online max only)."""
     lib = load_library()
     if q.dtype != torch.bfloat16 or k.dtype != torch.bfloat16 or v.dtype != torch.bfloat16:
         raise ValueError("attn_fwd expects bf16 q/k/v (attention() recasts to bf16 first)")
@@ -154,15 +159,18 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
         n_split = min(int(forced), (Lk + 63) // 64) if forced else attn_plan(B, H, Lq, Lk, D)
     ws_bytes = lib.cp25_attn_workspace_bytes(B, H, Lq, n_split)
     ws = torch.empty(((ws_bytes + 15) // 16 * 4,), dtype=torch.float32, device=q.device) if ws_bytes else None
-    rc = lib.cp25_attn_fwd_split(
+    qb, kb = (0.0, 0.0) if norm_bounds is None else (float(norm_bounds[0]), float(norm_bounds[1]))
+    if not (qb >= 0.0 and kb >= 0.0):
+        raise ValueError(f"norm_bounds must be >= 0, got {norm_bounds}")
+    rc = lib.cp25_attn_fwd_bounded(
         _ptr(q), _ptr(k), _ptr(v), _ptr(out), B, H, Lq, Lk, D,
         _i64x3((q.stride(0), q.stride(1), q.stride(2))),
         _i64x3((k.stride(0), k.stride(1), k.stride(2))),
         _i64x3((v.stride(0), v.stride(1), v.stride(2))),
         _i64x3((out.stride(0), out.stride(1), out.stride(2))),
-        scale, int(n_split), _ptr(ws), ws_bytes, _stream(q.device),
+        scale, qb, kb, int(n_split), _ptr(ws), ws_bytes, _stream(q.device),
     )
-    _check("cp25_attn_fwd_split", rc)
+    _check("cp25_attn_fwd_bounded", rc)
     return out
 
 

@@ -229,6 +229,18 @@ class MinimalV1LVGDiT:
         self.w_ada2 = torch.stack([p[f"blocks.{i}.adaln_modulation_{m}.2.weight"]
                                    for i in range(cfg.num_blocks) for m in ("self_attn", "cross_attn", "mlp")], 0).float()
         self.w_final = p["final_layer.linear.weight"].float()
+        # per-block (max|q|, max|k|) bounds for the bounded-shift attention softmax: the q/k RMSNorm
+        # (minimal_v4_dit.py:355-358) leaves every head row with |x| <= sqrt(hd) * max|weight|, RoPE
+        # is a rotation; 2 % covers the two bf16 roundings. One host read per weight, at load time.
+        hd = cfg.head_dim
+
+        def nb(w: torch.Tensor) -> float:
+            return float(w.float().abs().max()) * hd ** 0.5 * 1.02
+
+        self.attn_bounds = [(nb(p[f"blocks.{i}.self_attn.q_norm.weight"]), nb(p[f"blocks.{i}.self_attn.k_norm.weight"]))
+                            for i in range(cfg.num_blocks)]
+        self.xattn_bounds = [(nb(p[f"blocks.{i}.cross_attn.q_norm.weight"]),
+                              nb(p[f"blocks.{i}.cross_attn.k_norm.weight"])) for i in range(cfg.num_blocks)]
         self._rope_cache.clear()
         if D % 512:
             raise ValueError("model_channels must be a multiple of 512")
@@ -481,7 +493,8 @@ class MinimalV1LVGDiT:
                 vv = qkv.view(n, B, 3 * D)[:, :, 2 * D:].view(n, B, H, hd).transpose(0, 1)
                 if ev is not None:
                     ev[0].record()
-                N.attn_fwd(q, kk, vv, out=o.view(n, B, H, hd).transpose(0, 1), softmax_scale=scale_attn)
+                N.attn_fwd(q, kk, vv, out=o.view(n, B, H, hd).transpose(0, 1), softmax_scale=scale_attn,
+                           norm_bounds=self.attn_bounds[i])
                 lk = kk.shape[1]
             else:
                 yield from self._cp_self_attention(i, h, o, cos, sin, n, B, cp, cp_size,
@@ -505,7 +518,8 @@ class MinimalV1LVGDiT:
             qc = F.linear(h.view(n * B, D), p[pre + "cross_attn.q_proj.weight"])
             N.head_rmsnorm_rope(qc, n_rows=n * B, B=B, H=H, head_off=0, weight=p[pre + "cross_attn.q_norm.weight"])
             o = torch.empty((n, B, D), dtype=BF16, device=self.device)
-            self._cross_attention(qc.view(n, B, H, hd), ctx.k[i], ctx.v[i], o.view(n, B, H, hd), geo, scale_attn)
+            self._cross_attention(qc.view(n, B, H, hd), ctx.k[i], ctx.v[i], o.view(n, B, H, hd), geo, scale_attn,
+                                  self.xattn_bounds[i])
             y = F.linear(o.view(n * B, D), p[pre + "cross_attn.output_proj.weight"])
             _, _, g_ca = mod(i, 1)
             sh, sc, _ = mod(i, 2)
@@ -531,14 +545,14 @@ class MinimalV1LVGDiT:
         return out.view(n, B, -1)
 
     def _cross_attention(self, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, o: torch.Tensor, geo: Geometry,
-                         scale: float) -> None:
+                         scale: float, norm_bounds=None) -> None:
         """Text cross-attention of this shard's queries q/o [n, B, H, hd] against k/v [B, Lc, H, hd].
         Multi-view context holds 512 tokens per view and each view's queries see only their own
         (MultiViewCrossAttention, multiview_dit.py:40-55); a shard may span view boundaries."""
         n = q.shape[0]
         n_ctx = k.shape[1] // 512 if k.shape[1] % 512 == 0 else 1
         if geo.n_views == 1 or n_ctx == 1:
-            N.attn_fwd(q.transpose(0, 1), k, v, out=o.transpose(0, 1), softmax_scale=scale)
+            N.attn_fwd(q.transpose(0, 1), k, v, out=o.transpose(0, 1), softmax_scale=scale, norm_bounds=norm_bounds)
             return
         if n_ctx != geo.n_views:
             raise ValueError(f"context has {n_ctx} x 512 tokens for {geo.n_views} views")
@@ -548,7 +562,8 @@ class MinimalV1LVGDiT:
             if a >= b:
                 continue
             ks = slice(vi * 512, (vi + 1) * 512)
-            N.attn_fwd(q[a:b].transpose(0, 1), k[:, ks], v[:, ks], out=o[a:b].transpose(0, 1), softmax_scale=scale)
+            N.attn_fwd(q[a:b].transpose(0, 1), k[:, ks], v[:, ks], out=o[a:b].transpose(0, 1), softmax_scale=scale,
+                       norm_bounds=norm_bounds)
 
     def _cp_self_attention(self, i: int, h: torch.Tensor, o: torch.Tensor, cos, sin, n: int, B: int, cp,
                            cp_size: int, e0=None):
@@ -576,7 +591,8 @@ class MinimalV1LVGDiT:
         kc, vc = kv_chunk_views(kv_all, cp_size * n, B, H, hd)
         q = qkv.view(n, B, 3 * D)[:, :, :D].view(n, B, H, hd).transpose(0, 1)
         # the library's key-range split plan: B = 1 launches at CP = 8 leave a ragged last round
-        N.attn_fwd(q, kc, vc, out=o.view(n, B, H, hd).transpose(0, 1), softmax_scale=hd ** -0.5)
+        N.attn_fwd(q, kc, vc, out=o.view(n, B, H, hd).transpose(0, 1), softmax_scale=hd ** -0.5,
+                   norm_bounds=self.attn_bounds[i])
 
     # ---------------------------------------------------------------- reference-compatible forward
     @torch.no_grad()

@@ -18,6 +18,12 @@
 //   * padded LDS rows (K 272 B, V 320 B) keep both the ds_read_b128 row reads of K and the transposed
 //     reads of V bank-conflict-free with every address a per-lane base + immediate;
 //   * the O rescale of the online softmax is skipped (exactly) when no row max of the wave grew;
+//   * bounded shift (cp25_attn_fwd_bounded): given bounds on the query and key norms, each query row
+//     uses the Cauchy-Schwarz bound m = |q_row| max|k| * scale as its softmax shift instead of a
+//     running max, so the softmax has no max reduction, no rescale and no max -> exp dependency.
+//     Softmax is shift invariant, so this is the same result up to rounding; the host launches that
+//     form only when max|q| max|k| * scale <= kMaxShift (log2 units), which keeps every row's largest
+//     term >= 2^-2m >= 2^-100 (the row max is >= -m by the same bound): inside the fp32/bf16 range;
 //   * grid remapped so the workgroups of one XCD share a (batch, head): their K/V stream hits in
 //     that XCD's L2 instead of HBM.
 // NaN inputs are not supported (built with -fno-honor-nans; the reference's flash kernels do not
@@ -37,6 +43,7 @@ constexpr int kQRows = 32;     // query rows per wave
 constexpr int kQBlk = kWaves * kQRows;  // 256 query rows per workgroup
 constexpr int kKBlk = 64;      // keys per tile
 constexpr int kThreads = kWaves * 64;
+constexpr float kMaxShift = 50.f;  // bounded-shift cap, log2 units (header)
 // LDS layout (bytes): [K0 | K1 | V0 | V1]. Padded rows instead of an XOR swizzle so every LDS read
 // is one per-lane base VGPR + a compile-time immediate (no per-tile address arithmetic):
 //   K rows 272 B (256 + 16): the 16 rows a ds_read_b128 lane group reads at one column land on 16
@@ -84,6 +91,7 @@ struct AttnArgs {
   float* o_part;    // nsplit > 1: [nsplit][B][H][Lq][128] fp32 partial O (normalised per split)
   float* lse_part;  // nsplit > 1: [nsplit][B][H][Lq] fp32 log2-sum-exp2 of the scaled scores
   float scale_log2; // softmax scale * log2(e)
+  float kbound;     // > 0: upper bound of |k| over all keys (bounded shift); 0: online max only
 #ifdef CP25_ATTN_PROBE
   unsigned long long* probe;  // [wg < 8][wave][tile - probe_t0 < 32][8] s_memtime stamps (lab build only)
   int probe_t0;
@@ -115,7 +123,8 @@ struct AttnArgs {
 // stages V. Buffer lifetimes: K(j) and V(j) live in buffer j&1; K(t+1), V(t) are read in phases 2t
 // and 2t+1; K(t+2) is written in phase 2t over K(t) (last read in 2t-1), V(t+1) in phase 2t+1 over
 // V(t-1) (last read in 2t-1).
-template <int kKind>  // 0: self-attention, 1: cross-attention (separate symbols in profiles)
+// kKind 0: self-attention, 1: cross-attention (separate symbols in profiles); kFixed: bounded shift
+template <int kKind, bool kFixed>
 __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
 
@@ -157,6 +166,19 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
     for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
   float m_run = -1e30f;
   float l_run = 0.f;
+  // bounded shift: m = |q_row| * kbound * scale_log2 (the host checked the cap on the norm bounds)
+  if constexpr (kFixed) {
+    float qq = 0.f;
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float x = static_cast<float>(qf[s][e]);
+        qq = fmaf(x, x, qq);
+      }
+    qq = wave_swap_sum(qq);  // the row's two lanes hold its two halves
+    m_run = sqrtf(qq) * a.kbound * a.scale_log2;
+  }
 
   const int ntiles = (Lk + kKBlk - 1) / kKBlk;
 
@@ -231,23 +253,39 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
           if (key >= Lk) S[kt][r] = -INFINITY;
         }
     }
-    // four independent v_max3 chains (this file builds with -fno-honor-nans: no canonicalising
-    // v_max before each fmaxf of an MFMA result)
-    float mc[4];
+    // S enters here: keeps the (otherwise dependency-free) bounded-shift exp work from being
+    // hoisted across the barrier into the MFMA phase, where it would double the live P registers
+    asm volatile("" : "+v"(S[0]), "+v"(S[1]));
+    if constexpr (!kFixed) {
+      // four independent v_max3 chains (this file builds with -fno-honor-nans: no canonicalising
+      // v_max before each fmaxf of an MFMA result)
+      float mc[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) mc[j] = fmaxf(S[0][j], S[1][j]);
+      for (int j = 0; j < 4; ++j) mc[j] = fmaxf(S[0][j], S[1][j]);
 #pragma unroll
-    for (int r = 4; r < 16; ++r) mc[r & 3] = fmaxf(fmaxf(mc[r & 3], S[0][r]), S[1][r]);
-    const float mx = wave_swap_max(fmaxf(fmaxf(fmaxf(mc[0], mc[1]), mc[2]), mc[3]));
-    const float m_new = fmaxf(m_run, mx * a.scale_log2);
-    if (__any(m_new > m_run)) {
-      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-      l_run *= alpha;
+      for (int r = 4; r < 16; ++r) mc[r & 3] = fmaxf(fmaxf(mc[r & 3], S[0][r]), S[1][r]);
+      const float mx = wave_swap_max(fmaxf(fmaxf(fmaxf(mc[0], mc[1]), mc[2]), mc[3]));
+      const float m_new = fmaxf(m_run, mx * a.scale_log2);
+      if (__any(m_new > m_run)) {
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        l_run *= alpha;
 #pragma unroll
-      for (int d = 0; d < 4; ++d)
+        for (int d = 0; d < 4; ++d)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
-      m_run = m_new;
+          for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+        m_run = m_new;
+      }
+    } else {
+      // contract guard: a norm bound below the real norms can only show as an overflowed row sum
+      // (moderate violations are still exact by shift invariance); poison the row (NaN) instead of
+      // returning a silently wrong one. Never taken under the contract.
+      if (__builtin_expect(__any(l_run > 3.0e38f), 0)) {
+        const float nan = __uint_as_float(0x7fc00000u);
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[d][r] = nan;
+      }
     }
     float psum = 0.f;
 #pragma unroll
@@ -342,7 +380,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
       ATTN_STAMP(t, 1);
       if (t + 1 < ntiles) {
         // the staged V(t+1) goes to LDS before the softmax: its LDS write drains under the VALU
-        // (+0.7 % measured against writing after the softmax)
+        // (+0.9 % measured against writing after the softmax)
         write_v(std::integral_constant<int, par ^ 1>{});
         softmax(t + 1);
         ATTN_STAMP(t, 5);
@@ -352,11 +390,12 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
       __syncthreads();
       ATTN_STAMP(t, 3);
     };
-    for (int t = 0; t < ntiles; t += 2) {
+    // pairs of tiles (constexpr buffer parity), then the odd last tile: one loop exit
+    for (int t = 0; t + 1 < ntiles; t += 2) {
       step(B0{}, t);
-      if (t + 1 >= ntiles) break;
       step(B1{}, t + 1);
     }
+    if (ntiles & 1) step(B0{}, ntiles - 1);
   } else {
     // group B: phase 2t softmax(t) + K(t+2) staging, phase 2t+1 MFMA
     auto step = [&](auto PAR, int t) __attribute__((always_inline)) {
@@ -372,11 +411,12 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
       __syncthreads();
       ATTN_STAMP(t, 3);
     };
-    for (int t = 0; t < ntiles; t += 2) {
+    // pairs of tiles (constexpr buffer parity), then the odd last tile: one loop exit
+    for (int t = 0; t + 1 < ntiles; t += 2) {
       step(B0{}, t);
-      if (t + 1 >= ntiles) break;
       step(B1{}, t + 1);
     }
+    if (ntiles & 1) step(B0{}, ntiles - 1);
   }
 
   // ---- epilogue: O = O^T / l, bf16, row q, d = 32db + 8g + 4hl + (0..3) ----
@@ -493,11 +533,14 @@ extern "C" void cp25_attn_probe_set(unsigned long long* probe, int t0) { g_probe
 
 static int attn_launch(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq, int Lk, int D,
                        const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
-                       const int64_t* o_strides, float softmax_scale, int n_split, void* workspace, size_t ws_bytes,
-                       hipStream_t stream) {
+                       const int64_t* o_strides, float softmax_scale, float q_norm_bound, float k_norm_bound,
+                       int n_split, void* workspace, size_t ws_bytes, hipStream_t stream) {
   if (D != kD) return CP25_ERR_DTYPE;
   if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0) return CP25_ERR_INVAL;
   if (!q || !k || !v || !o) return CP25_ERR_INVAL;
+  if (!(softmax_scale > 0.f) || !(q_norm_bound >= 0.f) || !(k_norm_bound >= 0.f) || q_norm_bound > 1e18f ||
+      k_norm_bound > 1e18f)
+    return CP25_ERR_INVAL;
   // rows must be 16-byte aligned for the vector loads / stores; head dim contiguous
   const int64_t* ss[4] = {q_strides, k_strides, v_strides, o_strides};
   for (int i = 0; i < 4; ++i)
@@ -531,16 +574,18 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
   a.o_part = n_split > 1 ? (float*)workspace : nullptr;
   a.lse_part = n_split > 1 ? (float*)workspace + (size_t)n_split * rows * kD : nullptr;
   a.scale_log2 = softmax_scale * 1.4426950408889634f;
+  a.kbound = k_norm_bound;
+  const bool fixed = q_norm_bound > 0.f && k_norm_bound > 0.f &&
+                     (double)q_norm_bound * k_norm_bound * a.scale_log2 <= (double)kMaxShift;
 #ifdef CP25_ATTN_PROBE
   a.probe = g_probe;
   a.probe_t0 = g_probe_t0;
 #endif
   const int64_t nwg = (int64_t)a.nqb * B * H * n_split;
   if (nwg > 0x7fffffff) return CP25_ERR_INVAL;
-  if (Lk <= 4096)
-    hipLaunchKernelGGL(attn_fwd_d128<1>, dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
-  else
-    hipLaunchKernelGGL(attn_fwd_d128<0>, dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
+  auto kernel = Lk <= 4096 ? (fixed ? attn_fwd_d128<1, true> : attn_fwd_d128<1, false>)
+                           : (fixed ? attn_fwd_d128<0, true> : attn_fwd_d128<0, false>);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
   CP25_LAUNCH_CHECK();
   if (n_split > 1) {
     const int64_t threads = rows * 32;
@@ -566,14 +611,23 @@ extern "C" int cp25_attn_fwd(const void* q, const void* k, const void* v, void* 
                              int Lk, int D, const int64_t* q_strides, const int64_t* k_strides,
                              const int64_t* v_strides, const int64_t* o_strides, float softmax_scale,
                              hipStream_t stream) {
-  return attn_launch(q, k, v, o, B, H, Lq, Lk, D, q_strides, k_strides, v_strides, o_strides, softmax_scale, 1,
-                     nullptr, 0, stream);
+  return attn_launch(q, k, v, o, B, H, Lq, Lk, D, q_strides, k_strides, v_strides, o_strides, softmax_scale, 0.f,
+                     0.f, 1, nullptr, 0, stream);
 }
 
 extern "C" int cp25_attn_fwd_split(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq,
                                    int Lk, int D, const int64_t* q_strides, const int64_t* k_strides,
                                    const int64_t* v_strides, const int64_t* o_strides, float softmax_scale,
                                    int n_split, void* workspace, size_t ws_bytes, hipStream_t stream) {
+  return attn_launch(q, k, v, o, B, H, Lq, Lk, D, q_strides, k_strides, v_strides, o_strides, softmax_scale, 0.f,
+                     0.f, n_split, workspace, ws_bytes, stream);
+}
+
+extern "C" int cp25_attn_fwd_bounded(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq,
+                                     int Lk, int D, const int64_t* q_strides, const int64_t* k_strides,
+                                     const int64_t* v_strides, const int64_t* o_strides, float softmax_scale,
+                                     float q_norm_bound, float k_norm_bound, int n_split, void* workspace,
+                                     size_t ws_bytes, hipStream_t stream) {
   return attn_launch(q, k, v, o, B, H, Lq, Lk, D, q_strides, k_strides, v_strides, o_strides, softmax_scale,
-                     n_split, workspace, ws_bytes, stream);
+                     q_norm_bound, k_norm_bound, n_split, workspace, ws_bytes, stream);
 }

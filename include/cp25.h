@@ -49,7 +49,21 @@ int cp25_attn_fwd_split(const void* q, const void* k, const void* v, void* o, in
                         const int64_t* o_strides, float softmax_scale, int n_split, void* workspace,
                         size_t ws_bytes, hipStream_t stream);
 
-/* Bytes of workspace cp25_attn_fwd_split needs (0 for n_split <= 1). */
+/* cp25_attn_fwd_split with caller-supplied upper bounds of the query and key norms:
+ * q_norm_bound >= max |q| and k_norm_bound >= max |k| over all rows (0 = unknown). When both are given
+ * and q_norm_bound * k_norm_bound * softmax_scale * log2(e) <= 50, each query row uses the
+ * Cauchy-Schwarz bound |q_row| * k_norm_bound * softmax_scale as its softmax shift (softmax is shift
+ * invariant) instead of a running row max: no max reduction and no output rescale per key tile. The
+ * cap keeps every row's largest term >= 2^-100, inside the fp32/bf16 range. Otherwise (or with a 0
+ * bound) this is cp25_attn_fwd_split. Same result as cp25_attn_fwd_split up to rounding. The DiT
+ * passes sqrt(D) * max|q_norm.weight| and sqrt(D) * max|k_norm.weight|: the q/k RMSNorm
+ * (minimal_v4_dit.py:355-358) bounds every normed row by them and RoPE preserves the norm. */
+int cp25_attn_fwd_bounded(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq, int Lk,
+                          int D, const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
+                          const int64_t* o_strides, float softmax_scale, float q_norm_bound, float k_norm_bound,
+                          int n_split, void* workspace, size_t ws_bytes, hipStream_t stream);
+
+/* Bytes of workspace cp25_attn_fwd_split / _bounded need (0 for n_split <= 1). */
 size_t cp25_attn_workspace_bytes(int B, int H, int Lq, int n_split);
 
 /* The key-range split the library picks for this shape on the current device (>= 1; a round model of

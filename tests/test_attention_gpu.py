@@ -133,3 +133,81 @@ def test_attn_plan_and_bad_split(device):
     q = torch.zeros(1, 64, 1, 128, dtype=torch.bfloat16, device=device)
     with pytest.raises(ValueError):
         N.attn_fwd(q, q, q, n_split=2)  # one 64-key tile cannot be split in two
+
+
+def _rms_rows(t, w):
+    """q/k rows as the DiT's q/k RMSNorm leaves them: x / rms(x) * w (bf16)."""
+    tf = t.float()
+    return (tf * torch.rsqrt(tf.pow(2).mean(-1, keepdim=True) + 1e-6) * w).to(torch.bfloat16)
+
+
+def _bounds(q, k):
+    return (q.float().norm(dim=-1).max().item(), k.float().norm(dim=-1).max().item())
+
+
+@pytest.mark.parametrize(
+    "B,H,Lq,Lk,n_split",
+    [(1, 1, 32, 64, 1), (2, 3, 300, 77, 1), (2, 2, 1000, 1030, 1), (1, 2, 513, 4100, 1), (1, 2, 777, 3000, 3),
+     (1, 1, 5, 3, 1)],
+)
+def test_attn_bounded_shift_matches_fp32(device, B, H, Lq, Lk, n_split):
+    """cp25_attn_fwd_bounded: the Cauchy-Schwarz shift |q| max|k| scale replaces the running max
+    (softmax shift invariance) — same tolerance vs fp32, and within bf16 rounding of the online form."""
+    g = torch.Generator(device="cpu").manual_seed(99 + Lq + Lk)
+    w = 0.5 + torch.rand(128, generator=g)
+    q = _rms_rows(torch.randn(B, Lq, H, 128, generator=g), w).to(device)
+    k = _rms_rows(torch.randn(B, Lk, H, 128, generator=g), w).to(device)
+    v = torch.randn(B, Lk, H, 128, generator=g).to(device, torch.bfloat16)
+    nb = _bounds(q, k)
+    o = N.attn_fwd(q, k, v, n_split=n_split, norm_bounds=nb)
+    o_online = N.attn_fwd(q, k, v, n_split=n_split)
+    torch.cuda.synchronize()
+    ref = ref_attention(q, k, v)
+    assert torch.isfinite(o.float()).all()
+    assert rel_l2(o, ref) <= TOL, rel_l2(o, ref)
+    # P is rounded to bf16 at a different shift in each form: two independent ~2.2e-3 errors (sqrt 2)
+    assert rel_l2(o, o_online) <= 1.5 * TOL, rel_l2(o, o_online)
+
+
+def test_attn_bounded_shift_near_cap(device):
+    """Norms putting the per-row shift just under the 50 (log2) cap: sharp softmax rows whose largest
+    term sits far below the shift still come out right."""
+    g = torch.Generator(device="cpu").manual_seed(5)
+    B, H, Lq, Lk = 1, 2, 300, 700
+    r = (48.0 * 128 ** 0.5 / 1.4426950408889634) ** 0.5  # |q| = |k| = r -> shift 48 (log2 units)
+    q = torch.randn(B, Lq, H, 128, generator=g)
+    k = torch.randn(B, Lk, H, 128, generator=g)
+    q = (q / q.norm(dim=-1, keepdim=True) * r * 0.999).to(device, torch.bfloat16)
+    k = (k / k.norm(dim=-1, keepdim=True) * r * 0.999).to(device, torch.bfloat16)
+    v = torch.randn(B, Lk, H, 128, generator=g).to(device, torch.bfloat16)
+    o = N.attn_fwd(q, k, v, norm_bounds=(r, r))
+    torch.cuda.synchronize()
+    ref = ref_attention(q, k, v)
+    assert torch.isfinite(o.float()).all()
+    assert rel_l2(o, ref) <= TOL, rel_l2(o, ref)
+
+
+def test_attn_bounded_shift_over_cap_is_online(device):
+    """Bounds whose shift would exceed the cap select the online-max kernel: bitwise the plain path."""
+    g = torch.Generator(device="cpu").manual_seed(6)
+    q, k, v = (torch.randn(1, 400, 2, 128, generator=g).to(device, torch.bfloat16) for _ in range(3))
+    o = N.attn_fwd(q, k, v, norm_bounds=(1e3, 1e3))
+    o_plain = N.attn_fwd(q, k, v)
+    torch.cuda.synchronize()
+    assert torch.equal(o, o_plain)
+    with pytest.raises(ValueError):
+        N.attn_fwd(q, k, v, norm_bounds=(-1.0, 1.0))
+
+
+def test_attn_bounded_shift_violated_bound_is_loud(device):
+    """A caller bound far below the real norms overflows the row sum: the guard poisons the row
+    (non-finite output) instead of returning a silently wrong one."""
+    g = torch.Generator(device="cpu").manual_seed(8)
+    u = torch.randn(128, generator=g)
+    u = u / u.norm() * 40.0
+    q = u.expand(1, 64, 1, 128).contiguous().to(device, torch.bfloat16)
+    k = u.expand(1, 128, 1, 128).contiguous().to(device, torch.bfloat16)
+    v = torch.randn(1, 128, 1, 128, generator=g).to(device, torch.bfloat16)
+    o = N.attn_fwd(q, k, v, norm_bounds=(1.0, 1.0))
+    torch.cuda.synchronize()
+    assert not torch.isfinite(o.float()).all()

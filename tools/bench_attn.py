@@ -1,6 +1,6 @@
 """Micro-benchmark of cp25_attn_fwd at the DiT's shapes (timed with HIP events on the launch stream).
 
-usage: python tools/bench_attn.py [--L 109120] [--B 2] [--H 16] [--iters 5]
+usage: python tools/bench_attn.py [--L 109120] [--B 2] [--H 16] [--iters 5] [--bounded]
 Prints one JSON line per shape: ms per launch and TFLOP/s (4*B*H*Lq*Lk*D algorithmic FLOP).
 """
 import argparse
@@ -27,6 +27,10 @@ def main():
                     help="q/k/v as strided views of a token-major [L, B, 3*H*128] QKV buffer (the DiT's layout)")
     ap.add_argument("--zeros", action="store_true", help="zero-filled inputs (DVFS reference point)")
     ap.add_argument("--split", type=int, default=0, help="key-range split (0 = the library's plan)")
+    ap.add_argument("--bounded", action="store_true",
+                    help="RMS-normalised q/k rows (as the DiT's q/k norm leaves them) and their norm bounds: the "
+                         "bounded-shift softmax (cp25_attn_fwd_bounded)")
+    ap.add_argument("--normed", action="store_true", help="RMS-normalised q/k rows without passing the bounds")
     ap.add_argument("--lib", default="", help="lab build of libcp25.so to load instead of the in-tree one")
     a = ap.parse_args()
     if a.lib:
@@ -46,28 +50,34 @@ def main():
     if a.zeros:
         for t in (q, k, v):
             t.zero_()
+    nb = None
+    if a.bounded or a.normed:
+        for t in (q, k):  # RMSNorm with unit weight, in place, per head row
+            t.copy_((t.float() * torch.rsqrt(t.float().pow(2).mean(-1, keepdim=True) + 1e-6)).to(torch.bfloat16))
+        nb = (128 ** 0.5 * 1.02, 128 ** 0.5 * 1.02) if a.bounded else None
     # correctness of the loaded build on a small shape (ragged length) vs fp32 math
     gc = torch.Generator(device=dev).manual_seed(1)
     qc, kc, vc = (torch.randn(1, 1000, 2, 128, device=dev, generator=gc).to(torch.bfloat16) for _ in range(3))
     ref = torch.softmax(torch.einsum("bqhd,bkhd->bhqk", qc.float(), kc.float()) * 128 ** -0.5, -1)
     ref = torch.einsum("bhqk,bkhd->bqhd", ref, vc.float())
-    oc = N.attn_fwd(qc, kc, vc, n_split=1).float()
+    ncb = (qc.float().norm(dim=-1).max().item(), kc.float().norm(dim=-1).max().item()) if a.bounded else None
+    oc = N.attn_fwd(qc, kc, vc, n_split=1, norm_bounds=ncb).float()
     check = float((oc - ref).norm() / ref.norm())
     ns = a.split or N.attn_plan(a.B, a.H, a.L, Lk)
-    o = N.attn_fwd(q, k, v, n_split=ns)
+    o = N.attn_fwd(q, k, v, n_split=ns, norm_bounds=nb)
     torch.cuda.synchronize()
     st = torch.cuda.current_stream()
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     e0.record(st)
     for _ in range(a.iters):
-        N.attn_fwd(q, k, v, out=o, n_split=ns)
+        N.attn_fwd(q, k, v, out=o, n_split=ns, norm_bounds=nb)
     e1.record(st)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
     flop = 4.0 * a.B * a.H * a.L * Lk * 128
     print(json.dumps({"kernel": "attn_fwd", "B": a.B, "H": a.H, "Lq": a.L, "Lk": Lk, "fused": a.fused,
-                      "zeros": a.zeros, "split": ns, "iters": a.iters, "lib": os.path.basename(a.lib) or "libcp25.so", "ms": ms,
+                      "zeros": a.zeros, "bounded": a.bounded, "normed": a.normed or a.bounded, "split": ns, "iters": a.iters, "lib": os.path.basename(a.lib) or "libcp25.so", "ms": ms,
                       "tflops": flop / ms / 1e9, "check_rel_l2": check}))
 
 
