@@ -38,11 +38,14 @@ def main():
         q, k, v = (t.to(torch.bfloat16) for t in (q, k, v))
         ref = torch.softmax(torch.einsum("bqhd,bkhd->bhqk", q.float(), k.float()) * 128 ** -0.5, -1)
         ref = torch.einsum("bhqk,bkhd->bqhd", ref, v.float())
-        out = N.attn_fwd(q, k, v, n_split=ns).float()
-        rel = float((out - ref).norm() / ref.norm())
-        ok = rel < 4e-3 and bool(torch.isfinite(out).all())
-        bad += not ok
-        print(json.dumps({"B": B, "H": H, "Lq": Lq, "Lk": Lk, "split": ns, "scale": scale, "rel_l2": rel, "ok": ok}))
+        nb = (q.float().norm(dim=-1).max().item(), k.float().norm(dim=-1).max().item())
+        for bounds in (None, nb):  # online max, bounded shift
+            out = N.attn_fwd(q, k, v, n_split=ns, norm_bounds=bounds).float()
+            rel = float((out - ref).norm() / ref.norm())
+            ok = rel < 4e-3 and bool(torch.isfinite(out).all())
+            bad += not ok
+            print(json.dumps({"B": B, "H": H, "Lq": Lq, "Lk": Lk, "split": ns, "scale": scale,
+                              "bounded": bounds is not None, "rel_l2": rel, "ok": ok}))
     sys.exit(1 if bad else 0)
 
 

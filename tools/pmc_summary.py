@@ -11,7 +11,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNEL = "attn_fwd_d128<0>"
+KERNEL = "attn_fwd_d128<0"  # self-attention instantiations (<0, true>: bounded shift)
 FLOP = 4.0 * 2 * 16 * 109120 * 109120 * 128
 ALGO_BYTES = 4 * 2 * 16 * 109120 * 128 * 2  # Q, K, V read once, O written once (bf16)
 
