@@ -23,16 +23,23 @@ def main():
     ap.add_argument("--B", type=int, default=2)
     ap.add_argument("--H", type=int, default=16)
     ap.add_argument("--t0", type=int, default=200)
+    ap.add_argument("--bounded", action="store_true", help="RMS-normed q/k + cp25_attn_fwd_bounded (the DiT's form)")
     ap.add_argument("--lib", default=os.path.join(ROOT, "tools", "lab", "libattn_probe.so"))
     a = ap.parse_args()
     lib = ctypes.CDLL(a.lib)
     P = ctypes.c_void_p
     lib.cp25_attn_fwd.argtypes = [P, P, P, P] + [ctypes.c_int] * 5 + [P] * 4 + [ctypes.c_float, P]
     lib.cp25_attn_fwd.restype = ctypes.c_int
+    lib.cp25_attn_fwd_bounded.argtypes = [P, P, P, P] + [ctypes.c_int] * 5 + [P] * 4 + [ctypes.c_float] * 3 + \
+        [ctypes.c_int, P, ctypes.c_size_t, P]
+    lib.cp25_attn_fwd_bounded.restype = ctypes.c_int
     lib.cp25_attn_probe_set.argtypes = [P, ctypes.c_int]
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     q, k, v = (torch.randn(a.B, a.L, a.H, 128, device=dev, generator=g).to(torch.bfloat16) for _ in range(3))
+    if a.bounded:
+        for t in (q, k):
+            t.copy_((t.float() * torch.rsqrt(t.float().pow(2).mean(-1, keepdim=True) + 1e-6)).to(torch.bfloat16))
     o = torch.empty_like(q)
     probe = torch.zeros(8 * 8 * 32 * 8, dtype=torch.int64, device=dev)
 
@@ -43,8 +50,14 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
 
     def run():
-        rc = lib.cp25_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), a.B, a.H, a.L, a.L, 128,
-                               *[ctypes.cast(s, P) for s in st], 128 ** -0.5, stream)
+        if a.bounded:
+            nb = 128 ** 0.5 * 1.02
+            rc = lib.cp25_attn_fwd_bounded(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), a.B, a.H, a.L, a.L,
+                                           128, *[ctypes.cast(s, P) for s in st], 128 ** -0.5, nb, nb, 1, None, 0,
+                                           stream)
+        else:
+            rc = lib.cp25_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), a.B, a.H, a.L, a.L, 128,
+                                   *[ctypes.cast(s, P) for s in st], 128 ** -0.5, stream)
         assert rc == 0, rc
 
     lib.cp25_attn_probe_set(None, 0)
@@ -70,14 +83,16 @@ def main():
             "ph2": (t[..., 2] - t[..., 1]).mean(),
             "bar2": (t[..., 3] - t[..., 2]).mean(),
         }
-        # softmax-phase split: softmax VALU | wait for the staged loads + LDS write | load issue
-        sm_start = t[:, :, 1:, 1] if name == "A" else t[:, :, 1:, 3 - 3] * 0 + np.concatenate(
-            [t[:, :, :1, 3] * 0, t[:, :, :-1, 3]], axis=2)[:, :, 1:]
-        d["softmax_valu"] = (t[:, :, 1:, 4] - sm_start).mean()
-        d["stage_wait_write"] = (t[:, :, 1:, 5] - t[:, :, 1:, 4]).mean()
+        # softmax-phase split: staged LDS write + softmax VALU | load issue for the next staging
+        if name == "A":  # stamps 1 -> write_v, softmax -> 5 -> load_tile -> 2
+            d["write_softmax"] = (t[:, :, :, 5] - t[:, :, :, 1]).mean()
+            d["load_issue"] = (t[:, :, :, 2] - t[:, :, :, 5]).mean()
+        else:  # stamps 3 (previous tile) -> write_k, softmax -> 4 -> load_tile -> 0
+            d["write_softmax"] = (t[:, :, 1:, 4] - t[:, :, :-1, 3]).mean()
+            d["load_issue"] = (t[:, :, 1:, 0] - t[:, :, 1:, 4]).mean()
         res[name] = {k: round(float(x), 1) for k, x in d.items()}
     res["note"] = ("A: ph1 = MFMA phase, ph2 = softmax; B: ph1 = softmax, ph2 = MFMA (cycles of s_memtime); "
-                   "softmax_valu / stage_wait_write split the softmax phase")
+                   "write_softmax / load_issue split the softmax phase")
     print(json.dumps(res))
 
 
