@@ -7,7 +7,7 @@ buffer with this rank's shard repeated N times (same bytes written, no xGMI traf
 time per forward is therefore the rank's compute with zero-cost communication; compare it with
 (CP = 1 forward time) / N to see what the lanes cost, and add the exposed all-gather time for a
 real N-GPU estimate. Prints one JSON line per N.
-usage: python tools/sim_cp_rank.py [--cp 2 4 8] [--iters 2]
+usage: python tools/sim_cp_rank.py [--cp 2 4 8] [--iters 2] [--model 14B/pre-trained]
 """
 import argparse
 import faulthandler
@@ -32,7 +32,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cp", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--iters", type=int, default=2)
-    ap.add_argument("--blocks", type=int, default=28)
+    ap.add_argument("--model", default="2B/post-trained", help="net_config.MODELS key (14B: BASELINE config 3)")
+    ap.add_argument("--blocks", type=int, default=0, help="0 = the model's own block count")
     ap.add_argument("--gather", default="loop", choices=["expand", "loop", "none"],
                     help="how the fake gather fills the buffer (debug)")
     ap.add_argument("--trace", action="store_true", help="debug: event after every op; on a hang print the "
@@ -43,7 +44,9 @@ def main():
     a = ap.parse_args()
     faulthandler.dump_traceback_later(90, repeat=True)  # a stuck host shows where
     dev = torch.device("cuda:0")
-    cfg = MODELS["2B/post-trained"][0].replace(num_blocks=a.blocks)
+    cfg = MODELS[a.model][0]
+    if a.blocks:
+        cfg = cfg.replace(num_blocks=a.blocks)
     net = MinimalV1LVGDiT(cfg, device=dev)
     net.load_state_dict(init_state_dict(cfg, seed=0, device=dev))
     net.force_lanes = a.force_lanes
@@ -126,7 +129,7 @@ def main():
             net.forward_tokens(rows, t_B_T, ctx, geo)
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
-        print(json.dumps({"cp": n, "gather": a.gather, "blocks": a.blocks, "tokens_per_rank": geo.n_tok,
+        print(json.dumps({"model": a.model, "cp": n, "gather": a.gather, "blocks": cfg.num_blocks, "tokens_per_rank": geo.n_tok,
                           "forward_s": min(ts), "forward_s_all": ts}), flush=True)
 
 
