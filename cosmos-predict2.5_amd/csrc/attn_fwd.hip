@@ -18,12 +18,13 @@
 //   * padded LDS rows (K 272 B, V 320 B) keep both the ds_read_b128 row reads of K and the transposed
 //     reads of V bank-conflict-free with every address a per-lane base + immediate;
 //   * the O rescale of the online softmax is skipped (exactly) when no row max of the wave grew;
-//   * bounded shift (cp25_attn_fwd_bounded): given bounds on the query and key norms, each query row
-//     uses the Cauchy-Schwarz bound m = |q_row| max|k| * scale as its softmax shift instead of a
-//     running max, so the softmax has no max reduction, no rescale and no max -> exp dependency.
-//     Softmax is shift invariant, so this is the same result up to rounding; the host launches that
-//     form only when max|q| max|k| * scale <= kMaxShift (log2 units), which keeps every row's largest
-//     term >= 2^-2m >= 2^-100 (the row max is >= -m by the same bound): inside the fp32/bf16 range;
+//   * bounded shift (cp25_attn_fwd_bounded): given bounds on the query and key norms, every score of
+//     query row q lies in [-b, b] with b = |q_row| max|k| * scale (Cauchy-Schwarz, log2 units), so a
+//     fixed per-row shift m = max(b - kTop, 0) replaces the running max: the softmax has no max
+//     reduction, no rescale and no max -> exp dependency. Softmax is shift invariant, so this is the
+//     same result up to rounding, as long as every term stays in range: s - m <= kTop (no overflow of
+//     the row sum) and the row's largest term >= 2^(-b - m) >= 2^-100 (the row max is >= -b). Both
+//     hold for b <= kMaxBound; the host launches this form only when max|q| max|k| * scale is under it;
 //   * grid remapped so the workgroups of one XCD share a (batch, head): their K/V stream hits in
 //     that XCD's L2 instead of HBM.
 // NaN inputs are not supported (built with -fno-honor-nans; the reference's flash kernels do not
@@ -43,7 +44,8 @@ constexpr int kQRows = 32;     // query rows per wave
 constexpr int kQBlk = kWaves * kQRows;  // 256 query rows per workgroup
 constexpr int kKBlk = 64;      // keys per tile
 constexpr int kThreads = kWaves * 64;
-constexpr float kMaxShift = 50.f;  // bounded-shift cap, log2 units (header)
+constexpr float kTop = 60.f;        // bounded shift: largest exponent a term may reach (log2 units)
+constexpr float kMaxBound = 80.f;   // bounded shift: largest score bound b (2 b - kTop <= 100)
 // LDS layout (bytes): [K0 | K1 | V0 | V1]. Padded rows instead of an XOR swizzle so every LDS read
 // is one per-lane base VGPR + a compile-time immediate (no per-tile address arithmetic):
 //   K rows 272 B (256 + 16): the 16 rows a ds_read_b128 lane group reads at one column land on 16
@@ -177,7 +179,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
         qq = fmaf(x, x, qq);
       }
     qq = wave_swap_sum(qq);  // the row's two lanes hold its two halves
-    m_run = sqrtf(qq) * a.kbound * a.scale_log2;
+    m_run = fmaxf(sqrtf(qq) * a.kbound * a.scale_log2 - kTop, 0.f);
   }
 
   const int ntiles = (Lk + kKBlk - 1) / kKBlk;
@@ -576,7 +578,7 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
   a.scale_log2 = softmax_scale * 1.4426950408889634f;
   a.kbound = k_norm_bound;
   const bool fixed = q_norm_bound > 0.f && k_norm_bound > 0.f &&
-                     (double)q_norm_bound * k_norm_bound * a.scale_log2 <= (double)kMaxShift;
+                     (double)q_norm_bound * k_norm_bound * a.scale_log2 <= (double)kMaxBound;
 #ifdef CP25_ATTN_PROBE
   a.probe = g_probe;
   a.probe_t0 = g_probe_t0;

@@ -51,10 +51,11 @@ int cp25_attn_fwd_split(const void* q, const void* k, const void* v, void* o, in
 
 /* cp25_attn_fwd_split with caller-supplied upper bounds of the query and key norms:
  * q_norm_bound >= max |q| and k_norm_bound >= max |k| over all rows (0 = unknown). When both are given
- * and q_norm_bound * k_norm_bound * softmax_scale * log2(e) <= 50, each query row uses the
- * Cauchy-Schwarz bound |q_row| * k_norm_bound * softmax_scale as its softmax shift (softmax is shift
- * invariant) instead of a running row max: no max reduction and no output rescale per key tile. The
- * cap keeps every row's largest term >= 2^-100, inside the fp32/bf16 range. Otherwise (or with a 0
+ * and b = q_norm_bound * k_norm_bound * softmax_scale * log2(e) <= 80, every score of a row lies in
+ * [-b_row, b_row] (Cauchy-Schwarz, b_row from the row's own |q|), so the row uses the fixed softmax
+ * shift max(b_row - 60, 0) (softmax is shift invariant) instead of a running row max: no max
+ * reduction and no output rescale per key tile. Every term stays within [2^-100, 2^60], inside the
+ * fp32/bf16 range. Otherwise (or with a 0
  * bound) this is cp25_attn_fwd_split. Same result as cp25_attn_fwd_split up to rounding. The DiT
  * passes sqrt(D) * max|q_norm.weight| and sqrt(D) * max|k_norm.weight|: the q/k RMSNorm
  * (minimal_v4_dit.py:355-358) bounds every normed row by them and RoPE preserves the norm. */

@@ -169,12 +169,12 @@ def test_attn_bounded_shift_matches_fp32(device, B, H, Lq, Lk, n_split):
     assert rel_l2(o, o_online) <= 1.5 * TOL, rel_l2(o, o_online)
 
 
-def test_attn_bounded_shift_near_cap(device):
-    """Norms putting the per-row shift just under the 50 (log2) cap: sharp softmax rows whose largest
-    term sits far below the shift still come out right."""
+@pytest.mark.parametrize("bound", [48.0, 78.0])
+def test_attn_bounded_shift_near_cap(device, bound):
+    """Score bounds b up to the 80 (log2) cap: the shift max(b - 60, 0) keeps sharp rows right."""
     g = torch.Generator(device="cpu").manual_seed(5)
     B, H, Lq, Lk = 1, 2, 300, 700
-    r = (48.0 * 128 ** 0.5 / 1.4426950408889634) ** 0.5  # |q| = |k| = r -> shift 48 (log2 units)
+    r = (bound * 128 ** 0.5 / 1.4426950408889634) ** 0.5  # |q| = |k| = r -> b = bound (log2 units)
     q = torch.randn(B, Lq, H, 128, generator=g)
     k = torch.randn(B, Lk, H, 128, generator=g)
     q = (q / q.norm(dim=-1, keepdim=True) * r * 0.999).to(device, torch.bfloat16)
@@ -185,6 +185,28 @@ def test_attn_bounded_shift_near_cap(device):
     ref = ref_attention(q, k, v)
     assert torch.isfinite(o.float()).all()
     assert rel_l2(o, ref) <= TOL, rel_l2(o, ref)
+
+
+def test_attn_bounded_shift_extremes(device):
+    """Rows whose every score sits at +b or at -b (b = 78, keys parallel / antiparallel to the query):
+    the terms reach 2^60 and 2^-96 and both rows must still average V exactly."""
+    g = torch.Generator(device="cpu").manual_seed(11)
+    r = (78.0 * 128 ** 0.5 / 1.4426950408889634) ** 0.5
+    u = torch.randn(128, generator=g)
+    u = u / u.norm() * r * 0.999
+    Lq, Lk = 64, 200
+    q = torch.randn(1, Lq, 1, 128, generator=g)
+    q = q / q.norm(dim=-1, keepdim=True) * r * 0.999
+    q[0, 0, 0], q[0, 1, 0] = u, -u
+    k = u.expand(1, Lk, 1, 128).clone()
+    q, k = q.to(device, torch.bfloat16), k.to(device, torch.bfloat16)
+    v = torch.randn(1, Lk, 1, 128, generator=g).to(device, torch.bfloat16)
+    o = N.attn_fwd(q, k, v, norm_bounds=(r, r))
+    torch.cuda.synchronize()
+    mean_v = v.float().mean(1)[0, 0]
+    for row in (0, 1):
+        assert torch.isfinite(o[0, row, 0].float()).all()
+        assert rel_l2(o[0, row, 0], mean_v) <= TOL, (row, rel_l2(o[0, row, 0], mean_v))
 
 
 def test_attn_bounded_shift_over_cap_is_online(device):
