@@ -66,6 +66,7 @@ SIGNATURES = {
     "cp25_conv3d": [ctypes.POINTER(ctypes.c_void_p), _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I,
                     _I, _I, _I, _I, _I, _I, _P],
     "cp25_rms_norm_silu": [_P, _P, _P, _I64, _I, _I, _P],
+    "cp25_softmax_rows": [_P, _I64, _I, _I64, _F, _P, _I64, _P],
 }
 
 
@@ -320,4 +321,20 @@ def rms_norm_silu(x: torch.Tensor, gamma: torch.Tensor, silu: bool = True, out: 
         raise ValueError("rms_norm_silu expects a contiguous channels-last tensor")
     rc = lib.cp25_rms_norm_silu(_ptr(x), _ptr(gamma), _ptr(out), x.numel() // C, C, int(silu), _stream(x.device))
     _check("cp25_rms_norm_silu", rc)
+    return out
+
+
+def softmax_rows(s: torch.Tensor, scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bf16 softmax(s * scale) over the last dim of a 2-D fp32 score matrix (cp25_softmax_rows)."""
+    lib = load_library()
+    if s.dtype != torch.float32 or s.dim() != 2 or s.stride(1) != 1:
+        raise ValueError("softmax_rows expects a row-major 2-D fp32 tensor")
+    rows, cols = s.shape
+    if out is None:
+        out = torch.empty((rows, cols), dtype=torch.bfloat16, device=s.device)
+    if out.shape != s.shape or out.dtype != torch.bfloat16 or out.stride(1) != 1:
+        raise ValueError("softmax_rows: out must be a row-major bf16 tensor of the same shape")
+    rc = lib.cp25_softmax_rows(_ptr(s), rows, cols, s.stride(0), float(scale), _ptr(out), out.stride(0),
+                               _stream(s.device))
+    _check("cp25_softmax_rows", rc)
     return out

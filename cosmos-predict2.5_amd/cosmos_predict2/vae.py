@@ -10,8 +10,9 @@ re-laid-out for the GPU:
   kernel (zero frames are NULL), never a concatenated copy;
 * nearest-2x upsampling is fused into the conv's input gather, the upsample3d frame interleave into
   its epilogue, bias + residual adds into the conv epilogue; RMS_norm + SiLU is one HIP kernel.
-The single-head AttentionBlock core (C = 384 at h/8 x w/8) runs as two fp32 GEMMs + softmax on the
-device (round-1 interim; its 1x1 projections and norm are the HIP kernels).
+The single-head AttentionBlock core (C = 384 at h/8 x w/8) runs as S = Q K^T (library GEMM, fp32
+out), the HIP row softmax (cp25_softmax_rows, bf16 P) and P V (library GEMM); its 1x1 projections and
+norm are the HIP conv / norm kernels.
 
 Context parallel decode (set_context_parallel_group): the reference replicates the VAE on every rank;
 here each rank decodes a band of h/N latent rows (8h/N output rows) of every frame. A 3x3 conv needs
@@ -300,12 +301,14 @@ class WanVAE:
             kv_all = torch.empty((n,) + tuple(kv.shape), dtype=BF16, device=self.device)
             cpx.all_gather_into(kv_all, kv, group)
         for t in range(T):
-            q, k, v = qkv[t, :, :C].float(), qkv[t, :, C:2 * C].float(), qkv[t, :, 2 * C:].float()
+            # F.scaled_dot_product_attention(q, k, v) on bf16 (wan2pt1.py:251-254): fp32 scores of the
+            # bf16 operands (library GEMM), bf16 P from the HIP row softmax, P V with fp32 accumulation
+            q, k, v = qkv[t, :, :C], qkv[t, :, C:2 * C], qkv[t, :, 2 * C:]
             if kv_all is not None:
-                k = kv_all[:, t, :, :C].reshape(-1, C).float()
-                v = kv_all[:, t, :, C:].reshape(-1, C).float()
-            s = torch.matmul(q, k.t()) * (C ** -0.5)
-            o[t] = torch.matmul(torch.softmax(s, -1), v).to(BF16)
+                k = kv_all[:, t, :, :C].reshape(-1, C)
+                v = kv_all[:, t, :, C:].reshape(-1, C)
+            s = torch.mm(q, k.t(), out_dtype=torch.float32)
+            o[t] = torch.mm(N.softmax_rows(s, C ** -0.5), v.contiguous())
         o = o.view(T, H, W, C)
         return self.convs[p + ".proj"](_frames(o), T, H, W, residual=x)
 

@@ -272,6 +272,53 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
   return CP25_OK;
 }
 
+// ---------------------------------------------------------------- AttentionBlock softmax
+// P = softmax(S * scale) per row, fp32 scores in, bf16 probabilities out (the bf16 operand of the
+// P.V GEMM). One 256-thread workgroup per row: pass 1 keeps a per-thread running (max, sum) over a
+// strided slice of the row (float4 loads) and merges them across the block; pass 2 re-reads the row
+// (L2-resident: a 14 080-column row is 56 KB) and writes exp2((s - max) c) / sum. HBM-bound.
+__device__ __forceinline__ void ms_merge(float& m, float& l, float m2, float l2) {
+  const float mn = fmaxf(m, m2);
+  l = (m == -INFINITY ? 0.f : l * __builtin_amdgcn_exp2f(m - mn)) + (m2 == -INFINITY ? 0.f : l2 * __builtin_amdgcn_exp2f(m2 - mn));
+  m = mn;
+}
+
+__global__ void __launch_bounds__(256) softmax_rows_kernel(const float* __restrict__ s, int64_t ld_s, int cols,
+                                                           float c, unsigned short* __restrict__ p, int64_t ld_p,
+                                                           int vec) {
+  __shared__ float red_m[4], red_l[4];
+  const float* row = s + (int64_t)blockIdx.x * ld_s;
+  unsigned short* prow = p + (int64_t)blockIdx.x * ld_p;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n4 = vec ? cols >> 2 : 0;  // vec: rows 16-B (s) and 8-B (p) aligned
+  float m = -INFINITY, l = 0.f;
+  for (int i = tid; i < n4; i += 256) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(row + 4 * i);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ms_merge(m, l, v[e] * c, 1.f);
+  }
+  for (int i = 4 * n4 + tid; i < cols; i += 256) ms_merge(m, l, row[i] * c, 1.f);
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const float m2 = __shfl_xor(m, off), l2 = __shfl_xor(l, off);
+    ms_merge(m, l, m2, l2);
+  }
+  if (lane == 0) { red_m[wave] = m; red_l[wave] = l; }
+  __syncthreads();
+  m = red_m[0]; l = red_l[0];
+#pragma unroll
+  for (int w = 1; w < 4; ++w) ms_merge(m, l, red_m[w], red_l[w]);
+  const float inv = 1.f / l;
+  for (int i = tid; i < n4; i += 256) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(row + 4 * i);
+    u16x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = f2bf(__builtin_amdgcn_exp2f(v[e] * c - m) * inv);
+    *reinterpret_cast<u16x4*>(prow + 4 * i) = o;
+  }
+  for (int i = 4 * n4 + tid; i < cols; i += 256) prow[i] = f2bf(__builtin_amdgcn_exp2f(row[i] * c - m) * inv);
+}
+
 }  // namespace
 
 extern "C" int cp25_conv3d(const void* const* frames, int n_frames, const void* weight, const void* bias,
@@ -311,6 +358,17 @@ extern "C" int cp25_conv3d(const void* const* frames, int n_frames, const void* 
   CONV_CASE(64, 1) CONV_CASE(64, 2) CONV_CASE(64, 3) CONV_CASE(64, 4)
 #undef CONV_CASE
   return CP25_ERR_DTYPE;
+}
+
+extern "C" int cp25_softmax_rows(const float* s, int64_t rows, int cols, int64_t ld_s, float scale, void* p,
+                                 int64_t ld_p, hipStream_t stream) {
+  if (!s || !p || rows <= 0 || cols <= 0 || ld_s < cols || ld_p < cols || !(scale > 0.f)) return CP25_ERR_INVAL;
+  if (((uintptr_t)s & 3) || ((uintptr_t)p & 1) || rows > 0x7fffffff) return CP25_ERR_INVAL;
+  const int vec = !((uintptr_t)s & 15) && !((uintptr_t)p & 7) && !(ld_s & 3) && !(ld_p & 3);
+  hipLaunchKernelGGL(softmax_rows_kernel, dim3((unsigned)rows), dim3(256), 0, stream, s, ld_s, cols,
+                     scale * 1.4426950408889634f, (unsigned short*)p, ld_p, vec);
+  CP25_LAUNCH_CHECK();
+  return CP25_OK;
 }
 
 extern "C" int cp25_rms_norm_silu(const void* x, const void* gamma, void* y, int64_t n_pix, int C, int do_silu,

@@ -172,6 +172,14 @@ int cp25_conv3d(const void* const* frames, int n_frames, const void* weight, con
 int cp25_rms_norm_silu(const void* x, const void* gamma, void* y, int64_t n_pix, int C, int do_silu,
                        hipStream_t stream);
 
+/* p[r, :] = softmax(s[r, :] * scale) for `rows` rows of `cols` fp32 scores (row stride ld_s elements)
+ * -> bf16 probabilities (row stride ld_p); vector loads/stores when rows are 16-B / 8-B aligned. The
+ * AttentionBlock core of the VAE (single head, C = 384) runs as S = Q K^T (library GEMM, fp32 out),
+ * this kernel, and P V (library GEMM): replaces the softmax inside F.scaled_dot_product_attention in
+ * AttentionBlock.forward (wan2pt1.py:234-261). */
+int cp25_softmax_rows(const float* s, int64_t rows, int cols, int64_t ld_s, float scale, void* p, int64_t ld_p,
+                      hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -70,6 +70,22 @@ def test_rms_norm_silu(device):
     assert (o == ref[0]).float().mean().item() >= 0.99
 
 
+@pytest.mark.parametrize("rows,cols", [(7, 5), (64, 1000), (3, 14080), (5, 4099)])
+def test_softmax_rows(device, rows, cols):
+    """AttentionBlock softmax (cp25_softmax_rows): fp32 scores -> bf16 P, within one bf16 rounding of
+    torch.softmax in fp32; rows sum to 1 up to that rounding."""
+    g = torch.Generator().manual_seed(rows + cols)
+    s = (6 * torch.randn(rows, cols, generator=g)).to(device)
+    scale = 384 ** -0.5
+    p = N.softmax_rows(s, scale)
+    ref = torch.softmax(s * scale, -1)
+    assert p.dtype == torch.bfloat16
+    assert ((p.float() - ref).abs() <= 2 ** -8 * ref + 1e-30).all()
+    assert ((p.float().sum(-1) - 1).abs() <= 4e-3).all()
+    with pytest.raises(ValueError):
+        N.softmax_rows(s.to(torch.bfloat16), scale)
+
+
 @pytest.fixture(scope="module")
 def vae_pair():
     sd = init_vae_state_dict(seed=0)
