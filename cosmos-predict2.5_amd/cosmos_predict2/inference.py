@@ -1,8 +1,8 @@
 """Inference API: the reference's cosmos_predict2/inference.py (Inference(SetupArguments).generate).
 
-Inference(args).generate(samples, output_dir) -> list of written paths. Videos are written as a
-uint8 .npy array [T, H, W, 3] plus a frame-0 .png preview (no mp4 muxer ships in this image; the
-reference writes mp4 at 16 fps, inference.py:151-171, imaginaire/visualize/video.py). Guardrails and
+Inference(args).generate(samples, output_dir) -> list of written paths. Videos are written as .mp4
+at 16 fps like the reference (inference.py:151-171, imaginaire/visualize/video.py), by this build's
+own H.264 I_PCM muxer (video_io.py: no ffmpeg ships in this image). Guardrails and
 the Reason1 text encoder are outside this build: prompt embeddings come from the
 pipeline's `text_encoder` callable.
 """
@@ -17,20 +17,15 @@ import torch
 
 from .config import InferenceArguments, SetupArguments, is_rank0, path_to_str
 from .pipeline import Video2WorldInference
+from .video_io import write_mp4
 
 log = logging.getLogger("cosmos_predict2")
 
 
-def save_video(video_0_1_C_T_H_W: torch.Tensor, path_stem: str) -> str:
+def save_video(video_0_1_C_T_H_W: torch.Tensor, path_stem: str, fps: int = 16) -> str:
+    """[C, T, H, W] in [0, 1] -> <stem>.mp4 (uint8 frames, as save_img_or_video does)."""
     frames = (video_0_1_C_T_H_W * 255.0).clamp(0, 255).to(torch.uint8).permute(1, 2, 3, 0).cpu().numpy()
-    np.save(path_stem + ".npy", frames)
-    try:
-        from PIL import Image
-
-        Image.fromarray(frames[0]).save(path_stem + ".png")
-    except Exception:  # noqa: BLE001 - preview only
-        pass
-    return path_stem + ".npy"
+    return write_mp4(np.ascontiguousarray(frames), path_stem + ".mp4", fps=fps)
 
 
 class Inference:
@@ -78,4 +73,4 @@ class Inference:
             raise
         if self.rank0:
             return save_video((1.0 + video[0]) / 2, str(stem))
-        return str(stem) + ".npy"
+        return str(stem) + ".mp4"

@@ -195,8 +195,13 @@ class Video2WorldInference:
             ext = os.path.splitext(input_path)[1].lower()
             if ext in _IMAGE_EXTENSIONS:
                 vid = read_and_process_image(input_path, (h, w), frames)
+            elif ext in _VIDEO_EXTENSIONS:  # read_and_process_video (video2world.py:150-233)
+                from .video_io import read_mp4
+
+                vid = process_video_frames(torch.from_numpy(read_mp4(input_path)), (h, w), frames,
+                                           num_latent_conditional_frames)
             else:
-                raise ValueError(f"Unsupported file extension: {ext} (decode mp4 frames yourself and pass a tensor)")
+                raise ValueError(f"Unsupported file extension: {ext}")
         elif isinstance(input_path, torch.Tensor):
             vid = input_path
         else:
