@@ -39,6 +39,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=0, help="untimed videos before timing")
     ap.add_argument("--num-steps", type=int, default=35, help="UniPC steps (35 = the metric)")
     ap.add_argument("--frames", type=int, default=121)
+    ap.add_argument("--model", default="2B/post-trained",
+                    help="2B/post-trained: Karras, 36 evals (the metric); 2B/pre-trained: shift-5 linspace, 35 evals "
+                         "(SURVEY.md 8(d)'s second variant)")
     ap.add_argument("--resolution", default="704,1280")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -82,7 +85,8 @@ def main():
     _native.load_library()
     h, w = (int(x) for x in a.resolution.split(","))
     state_t = 1 + (a.frames - 1) // 4
-    pipe = Video2WorldInference("2B/post-trained", context_parallel_size=world, device=dev, state_t=state_t)
+    pipe = Video2WorldInference(a.model, context_parallel_size=world, device=dev, state_t=state_t)
+    karras = pipe.model.config.use_kerras_sigma_at_inference
     frames = pipe.model.tokenizer.get_pixel_num_frames(state_t)
     # conditioning "image": frame 0 random uint8, later frames zero (read_and_process_image layout)
     rng = np.random.RandomState(3)
@@ -132,7 +136,7 @@ def main():
 
     if rank == 0:
         ms = elapsed / a.steps * 1e3
-        valid = a.num_steps == 35 and a.frames == 121 and (h, w) == (704, 1280)
+        valid = a.num_steps == 35 and a.frames == 121 and (h, w) == (704, 1280) and a.model == "2B/post-trained"
         # HBM bytes per self-attention launch from the committed rocprofv3 PMC passes of this kernel
         # at this shape (tools/pmc_attn.sh, FETCH_SIZE x2 gfx950 correction + WRITE_SIZE); only the
         # CP = 1 metric shape was measured, so other shapes report null
@@ -155,8 +159,10 @@ def main():
             "dtype": "bf16",
             "data": "synthetic: seeded random 2B/VAE weights, random conditioning image, N(0,1) text embeddings",
             "config": {
-                "workload": f"Predict2.5-2B Image2World {h}x{w}x{frames}f, {a.num_steps} Karras UniPC steps "
-                            f"({a.num_steps + 1} evals x CFG 2, batched), VAE encode cond frame + decode {frames}f",
+                "workload": f"Predict2.5-2B Image2World {h}x{w}x{frames}f ({a.model}), {a.num_steps} "
+                            + (f"Karras UniPC steps ({a.num_steps + 1} evals" if karras else
+                               f"shift-5 UniPC steps ({a.num_steps} evals")
+                            + f" x CFG 2, batched), VAE encode cond frame + decode {frames}f",
                 "latent": [16, state_t, h // 8, w // 8],
                 "tokens": state_t * (h // 16) * (w // 16),
                 "global_batch": 1,
