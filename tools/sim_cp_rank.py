@@ -34,6 +34,9 @@ def main():
     ap.add_argument("--iters", type=int, default=2)
     ap.add_argument("--model", default="2B/post-trained", help="net_config.MODELS key (14B: BASELINE config 3)")
     ap.add_argument("--blocks", type=int, default=0, help="0 = the model's own block count")
+    ap.add_argument("--geometry", default="31,44,80", help="latent frames, patch rows, patch cols (T,Hp,Wp); "
+                    "multi-view: T = views x frames per view")
+    ap.add_argument("--views", type=int, default=1, help="views stacked along T (multi-view nets)")
     ap.add_argument("--gather", default="loop", choices=["expand", "loop", "none"],
                     help="how the fake gather fills the buffer (debug)")
     ap.add_argument("--trace", action="store_true", help="debug: event after every op; on a hang print the "
@@ -47,15 +50,17 @@ def main():
     cfg = MODELS[a.model][0]
     if a.blocks:
         cfg = cfg.replace(num_blocks=a.blocks)
+    T, Hp, Wp = (int(x) for x in a.geometry.split(","))
+    if a.views > 1:
+        cfg = cfg.replace(state_t=T // a.views)
     net = MinimalV1LVGDiT(cfg, device=dev)
     net.load_state_dict(init_state_dict(cfg, seed=0, device=dev))
     net.force_lanes = a.force_lanes
-    T, Hp, Wp = 31, 44, 80
     L = T * Hp * Wp
     g = torch.Generator(device=dev).manual_seed(0)
     nb = 1 if a.batch1 else 2
-    ctx = net.prepare_context(torch.randn(nb, 512, cfg.crossattn_proj_in_channels, device=dev, generator=g)
-                              .to(torch.bfloat16))
+    ctx = net.prepare_context(torch.randn(nb, 512 * a.views, cfg.crossattn_proj_in_channels, device=dev,
+                                          generator=g).to(torch.bfloat16))
     t_B_T = torch.full((nb, T), 0.877, device=dev)
     state = {"cp": 1}
 
@@ -106,7 +111,7 @@ def main():
     for n in a.cp:
         state["cp"] = n
         net.cp_group = None if n == 1 else object()
-        geo = Geometry(T=T, Hp=Hp, Wp=Wp, tok0=0, n_tok=L // n)
+        geo = Geometry(T=T, Hp=Hp, Wp=Wp, tok0=0, n_tok=L // n, n_views=a.views)
         rows = torch.randn(geo.n_tok, 1, 72, device=dev, generator=g).to(torch.bfloat16)
         print(f"cp {n}: warm-up forward", flush=True)
         net.forward_tokens(rows, t_B_T, ctx, geo)  # warm
@@ -129,7 +134,7 @@ def main():
             net.forward_tokens(rows, t_B_T, ctx, geo)
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
-        print(json.dumps({"model": a.model, "cp": n, "gather": a.gather, "blocks": cfg.num_blocks, "tokens_per_rank": geo.n_tok,
+        print(json.dumps({"model": a.model, "geometry": [T, Hp, Wp], "views": a.views, "cp": n, "gather": a.gather, "blocks": cfg.num_blocks, "tokens_per_rank": geo.n_tok,
                           "forward_s": min(ts), "forward_s_all": ts}), flush=True)
 
 
