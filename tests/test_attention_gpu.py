@@ -233,3 +233,30 @@ def test_attn_bounded_shift_violated_bound_is_loud(device):
     o = N.attn_fwd(q, k, v, norm_bounds=(1.0, 1.0))
     torch.cuda.synchronize()
     assert not torch.isfinite(o.float()).all()
+
+
+@pytest.mark.parametrize("bounded", [False, True])
+def test_attn_full_metric_shape_query_slice(device, bounded):
+    """BASELINE config 2's self-attention launch (B 2, H 16, L = Lk = 109 120, RMS-normed q/k as the
+    DiT feeds it): 384 query rows checked against fp32 attention over all 109 120 keys, and
+    V = const -> O = const for every row (the normalised weights sum to 1)."""
+    L, B, H = 109120, 2, 16
+    g = torch.Generator(device=device).manual_seed(3)
+    w = 0.5 + torch.rand(128, device=device, generator=g)
+    q = _rms_rows(torch.randn(B, L, H, 128, device=device, generator=g), w)
+    k = _rms_rows(torch.randn(B, L, H, 128, device=device, generator=g), w)
+    v = torch.randn(B, L, H, 128, device=device, generator=g).to(torch.bfloat16)
+    nb = _bounds(q, k) if bounded else None
+    o = N.attn_fwd(q, k, v, norm_bounds=nb)
+    rows = torch.randperm(L, generator=torch.Generator().manual_seed(4))[:384].to(device)
+    err = []
+    for b in range(B):
+        for h in range(H):
+            s = (q[b, rows, h].float() @ k[b, :, h].float().t()) * 128 ** -0.5
+            ref = torch.softmax(s, -1) @ v[b, :, h].float()
+            err.append(((o[b, rows, h].float() - ref).norm() / ref.norm()).item())
+    assert max(err) <= TOL, max(err)
+    vc = torch.full_like(v, 0.75)
+    oc = N.attn_fwd(q, k, vc, norm_bounds=nb)
+    torch.cuda.synchronize()
+    assert ((oc.float() - 0.75).abs() <= 0.75 * 2 ** -7).all()
