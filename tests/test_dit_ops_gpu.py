@@ -148,3 +148,22 @@ def test_unipc_bit_exact(device, karras, steps):
         xc = orc.step(v, t, xc)
         sch.step_(v.to(device), t)
         assert torch.equal(xg.cpu(), xc), f"step {i}: max diff {(xg.cpu() - xc).abs().max().item()}"
+
+
+def test_unipc_bit_exact_full_latent(device):
+    """The metric's whole latent (16 x 31 x 88 x 160 = 6.98 M elements), 35 Karras steps: the fused
+    HIP step stays bit-identical to the fp32 oracle trajectory at full size."""
+    n = 16 * 31 * 88 * 160
+    steps = 35
+    g = torch.Generator().manual_seed(9)
+    x0 = torch.randn(n, generator=g)
+    orc = UniPC(steps, shift=5.0, use_karras=True)
+    sch = FlowUniPCMultistepScheduler(shift=1)
+    sch.set_timesteps(steps, device=device, shift=5.0, use_kerras_sigma=True)
+    xg = sch.begin(x0.to(device))
+    xc = x0.clone()
+    for i, t in enumerate(orc.timesteps):
+        v = torch.sin(xc * 1.3 + i) * 0.7
+        xc = orc.step(v, t, xc)
+        sch.step_(v.to(device), t)
+    assert torch.equal(xg.cpu(), xc)
