@@ -109,6 +109,17 @@ def test_gelu(device):
     assert ok, eq
 
 
+def test_gelu_every_bf16_value(device):
+    """Exact-erf GELU over every finite bf16 input (65 024 values), against torch's fp32 evaluation."""
+    bits = torch.arange(0, 1 << 16, dtype=torch.int32).to(torch.int16).view(torch.bfloat16)
+    x = bits[torch.isfinite(bits.float())].to(device)
+    ref = F.gelu(x)
+    y = x.clone()
+    N.gelu_(y)
+    ok, eq = bf16_ulp_close(y, ref)
+    assert ok, eq
+
+
 def test_patchify_and_cfg_exact(device):
     T, Hp, Wp = 3, 4, 6
     L, hw = T * Hp * Wp, Hp * Wp
