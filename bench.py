@@ -43,6 +43,8 @@ def parse():
                     help="2B/post-trained: Karras, 36 evals (the metric); 2B/pre-trained: shift-5 linspace, 35 evals "
                          "(SURVEY.md 8(d)'s second variant)")
     ap.add_argument("--resolution", default="704,1280")
+    ap.add_argument("--linear-precision", default="bf16", choices=("bf16", "fp8"),
+                    help="fp8: the DiT block projections/MLP as fp8 MFMA GEMMs (config 5's option; not the metric)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--backend", default="nccl", help="process-group backend for N > 1 (nccl = RCCL; gloo only "
@@ -85,7 +87,8 @@ def main():
     _native.load_library()
     h, w = (int(x) for x in a.resolution.split(","))
     state_t = 1 + (a.frames - 1) // 4
-    pipe = Video2WorldInference(a.model, context_parallel_size=world, device=dev, state_t=state_t)
+    pipe = Video2WorldInference(a.model, context_parallel_size=world, device=dev, state_t=state_t,
+                                linear_precision=a.linear_precision)
     karras = pipe.model.config.use_kerras_sigma_at_inference
     frames = pipe.model.tokenizer.get_pixel_num_frames(state_t)
     # conditioning "image": frame 0 random uint8, later frames zero (read_and_process_image layout)
@@ -136,7 +139,8 @@ def main():
 
     if rank == 0:
         ms = elapsed / a.steps * 1e3
-        valid = a.num_steps == 35 and a.frames == 121 and (h, w) == (704, 1280) and a.model == "2B/post-trained"
+        valid = (a.num_steps == 35 and a.frames == 121 and (h, w) == (704, 1280) and a.model == "2B/post-trained"
+                 and a.linear_precision == "bf16")
         # HBM bytes per self-attention launch from the committed rocprofv3 PMC passes of this kernel
         # at this shape (tools/pmc_attn.sh, FETCH_SIZE x2 gfx950 correction + WRITE_SIZE); only the
         # CP = 1 metric shape was measured, so other shapes report null
@@ -156,7 +160,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" if a.linear_precision == "bf16" else "fp8 (block GEMMs) + bf16",
             "data": "synthetic: seeded random 2B/VAE weights, random conditioning image, N(0,1) text embeddings",
             "config": {
                 "workload": f"Predict2.5-2B Image2World {h}x{w}x{frames}f ({a.model}), {a.num_steps} "
@@ -167,6 +171,7 @@ def main():
                 "tokens": state_t * (h // 16) * (w // 16),
                 "global_batch": 1,
                 "parallelism": f"cp{world}",
+                "linear_precision": a.linear_precision,
                 "metric_config": valid,
             },
             "roofline": {

@@ -60,6 +60,8 @@ SIGNATURES = {
     "cp25_head_rmsnorm_rope": [_P, _I64, _I64, _I, _I, _I, _P, _P, _P, _P, _I64, _F, _P],
     "cp25_copy_rows": [_P, _I64, _P, _I64, _I64, _I64, _P],
     "cp25_gelu": [_P, _I64, _P],
+    "cp25_quant_fp8_rows": [_P, _P, _P, _I64, _I64, _P],
+    "cp25_gelu_quant_fp8": [_P, _P, _P, _I64, _I64, _P],
     "cp25_patchify": [_P, _P, _P, _P, _P, _I64, _I64, _I64, _P],
     "cp25_cfg_velocity": [_P, _I, _P, _P, _P, _F, _I, _P, _I64, _I64, _I64, _P],
     "cp25_unipc_step": [_P, _P, _P, _P, _P, _I64, ctypes.POINTER(UniPCParams), _P],
@@ -256,6 +258,20 @@ def gelu_(x: torch.Tensor) -> torch.Tensor:
         raise ValueError("gelu_ expects a contiguous bf16 tensor")
     _check("cp25_gelu", lib.cp25_gelu(_ptr(x), x.numel(), _stream(x.device)))
     return x
+
+
+def quant_fp8_rows(x: torch.Tensor, gelu: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Row-scaled fp8 (float8_e4m3fn) operand of x [M, K] bf16: returns (q [M, K], scale [M, 1] fp32) with
+    x ~= q * scale (of GELU(x) when gelu=True). cp25_quant_fp8_rows / cp25_gelu_quant_fp8."""
+    lib = load_library()
+    if x.dim() != 2 or not x.is_contiguous() or x.dtype != torch.bfloat16:
+        raise ValueError("quant_fp8_rows expects a contiguous 2-D bf16 tensor")
+    q = torch.empty(x.shape, dtype=torch.float8_e4m3fn, device=x.device)
+    s = torch.empty((x.shape[0], 1), dtype=torch.float32, device=x.device)
+    fn = lib.cp25_gelu_quant_fp8 if gelu else lib.cp25_quant_fp8_rows
+    _check("cp25_gelu_quant_fp8" if gelu else "cp25_quant_fp8_rows",
+           fn(_ptr(x), _ptr(q), _ptr(s), x.shape[0], x.shape[1], _stream(x.device)))
+    return q, s
 
 
 def patchify(xs: torch.Tensor, gt: Optional[torch.Tensor], frame_mask: torch.Tensor,

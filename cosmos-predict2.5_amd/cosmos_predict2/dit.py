@@ -195,6 +195,44 @@ class MinimalV1LVGDiT:
         self.force_lanes = False  # run the per-batch-entry lanes at CP = 1 too (CP parity tests)
         # optional list collecting (start, end, flop) HIP events around every self-attention launch
         self.attn_events: Optional[list] = None
+        # "bf16" (the reference's precision) or "fp8": the block projections and MLP as fp8 MFMA GEMMs
+        # with row-scaled activations and per-output-channel weight scales (config 5, see set_linear_precision)
+        self.linear_precision = "bf16"
+        self._fp8_w: Dict[str, Tuple[torch.Tensor, torch.Tensor]] = {}
+
+    def set_linear_precision(self, precision: str) -> None:
+        """"bf16" (default, the reference's arithmetic) or "fp8": the 28 blocks' q/k/v, output, cross-q,
+        cross-output and MLP projections run as hipBLASLt fp8 (OCP E4M3) MFMA GEMMs, activations quantised
+        per row by cp25_quant_fp8_rows (the MLP's fused with its GELU, cp25_gelu_quant_fp8), weights per
+        output channel (once, on first use). Embedders, AdaLN, the text projection and the final layer
+        stay bf16/fp32. The reference has no fp8 path: the cost is stated against the bf16 path
+        (DESIGN.md §4), not pinned to a reference output."""
+        if precision not in ("bf16", "fp8"):
+            raise ValueError(f"linear precision must be 'bf16' or 'fp8', got {precision!r}")
+        self.linear_precision = precision
+        self._fp8_w = {}
+
+    def _fp8_weight(self, key: str, w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        ent = self._fp8_w.get(key)
+        if ent is None:
+            fmax = torch.finfo(torch.float8_e4m3fn).max
+            wf = w.float()
+            sc = (wf.abs().amax(dim=1, keepdim=True) / fmax).clamp_min(torch.finfo(torch.float32).tiny)
+            w8 = (wf / sc).clamp(-fmax, fmax).to(torch.float8_e4m3fn)
+            ent = (w8, sc.t().contiguous())  # [N, K] fp8, [1, N] fp32
+            self._fp8_w[key] = ent
+        return ent
+
+    def _linear(self, x: torch.Tensor, w: torch.Tensor, key: str, gelu_in: bool = False) -> torch.Tensor:
+        """y = x w^T for a block projection (x [M, K] bf16 contiguous). bf16: hipBLASLt bf16 GEMM (GELU,
+        if asked, applied in place to x first). fp8: row-quantised x (GELU fused) times the fp8 weight."""
+        if self.linear_precision == "bf16":
+            if gelu_in:
+                N.gelu_(x)
+            return F.linear(x, w)
+        q, s = N.quant_fp8_rows(x, gelu=gelu_in)
+        w8, ws = self._fp8_weight(key, w)
+        return torch._scaled_mm(q, w8.t(), scale_a=s, scale_b=ws, out_dtype=BF16)
 
     # ---------------------------------------------------------------- loading
     def load_state_dict(self, state_dict: Dict[str, torch.Tensor], strict: bool = True) -> None:
@@ -216,6 +254,7 @@ class MinimalV1LVGDiT:
         cfg = self.cfg
         dev = self.device
         self.sd = {k: v.to(device=dev, dtype=shapes[k][1]).contiguous() for k, v in sd.items()}
+        self._fp8_w = {}
         D = cfg.model_channels
         p = self.sd
         # fused / stacked views used by the hot path
@@ -483,7 +522,7 @@ class MinimalV1LVGDiT:
             if self.attn_events is not None:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             if cp is None or cp_size == 1:
-                qkv = F.linear(h.view(n * B, D), self.w_qkv[i])  # [n*B, 3D]
+                qkv = self._linear(h.view(n * B, D), self.w_qkv[i], f"qkv.{i}")  # [n*B, 3D]
                 N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=0,
                                     weight=p[pre + "self_attn.q_norm.weight"], cos=cos, sin=sin)
                 N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=D,
@@ -503,7 +542,7 @@ class MinimalV1LVGDiT:
             if ev is not None:
                 ev[1].record()
                 self.attn_events.append((ev[0], ev[1], 4.0 * B * H * n * lk * hd))
-            y = F.linear(o.view(n * B, D), p[pre + "self_attn.output_proj.weight"])
+            y = self._linear(o.view(n * B, D), p[pre + "self_attn.output_proj.weight"], pre + "self_attn.output_proj")
             # ---- x += g_sa * y ; LN-mod for cross attention
             _, _, g_sa = mod(i, 0)
             sh, sc, _ = mod(i, 1)
@@ -515,21 +554,20 @@ class MinimalV1LVGDiT:
             h = N.ln_mod(x, sh, sc, x_st=x_st, x_sb=x_sb, y=y, gate=g_sa, x_out=x_new, **common)
             x = x_new
             # ---- cross attention
-            qc = F.linear(h.view(n * B, D), p[pre + "cross_attn.q_proj.weight"])
+            qc = self._linear(h.view(n * B, D), p[pre + "cross_attn.q_proj.weight"], pre + "cross_attn.q_proj")
             N.head_rmsnorm_rope(qc, n_rows=n * B, B=B, H=H, head_off=0, weight=p[pre + "cross_attn.q_norm.weight"])
             o = torch.empty((n, B, D), dtype=BF16, device=self.device)
             self._cross_attention(qc.view(n, B, H, hd), ctx.k[i], ctx.v[i], o.view(n, B, H, hd), geo, scale_attn,
                                   self.xattn_bounds[i])
-            y = F.linear(o.view(n * B, D), p[pre + "cross_attn.output_proj.weight"])
+            y = self._linear(o.view(n * B, D), p[pre + "cross_attn.output_proj.weight"], pre + "cross_attn.output_proj")
             _, _, g_ca = mod(i, 1)
             sh, sc, _ = mod(i, 2)
             x_new = torch.empty((n, B, D), dtype=BF16, device=self.device)
             h = N.ln_mod(x, sh, sc, x_st=B * D, x_sb=D, y=y, gate=g_ca, x_out=x_new, **common)
             x = x_new
             # ---- MLP
-            u = F.linear(h.view(n * B, D), p[pre + "mlp.layer1.weight"])
-            N.gelu_(u)
-            y = F.linear(u, p[pre + "mlp.layer2.weight"])
+            u = self._linear(h.view(n * B, D), p[pre + "mlp.layer1.weight"], pre + "mlp.layer1")
+            y = self._linear(u, p[pre + "mlp.layer2.weight"], pre + "mlp.layer2", gelu_in=True)
             del u
             _, _, gate_prev = mod(i, 2)
             if i + 1 < cfg.num_blocks:
@@ -575,7 +613,7 @@ class MinimalV1LVGDiT:
         p = self.sd
         pre = f"blocks.{i}."
         D, H, hd = cfg.model_channels, cfg.num_heads, cfg.head_dim
-        qkv = F.linear(h.view(n * B, D), self.w_qkv[i])  # [n*B, 3D]
+        qkv = self._linear(h.view(n * B, D), self.w_qkv[i], f"qkv.{i}")  # [n*B, 3D]
         N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=D, weight=p[pre + "self_attn.k_norm.weight"],
                             cos=cos, sin=sin)
         kv = torch.empty((n * B, 2 * D), dtype=BF16, device=self.device)

@@ -1,0 +1,131 @@
+// fp8 (OCP E4M3, gfx950's native fp8 format) activation quantisation for the DiT's fp8 linear layers
+// (BASELINE config 5, "fp8 MFMA"). The GEMMs themselves run on hipBLASLt's fp8 MFMA kernels through
+// torch._scaled_mm with a per-row activation scale and a per-output-channel weight scale; these
+// kernels produce the row-scaled activation operand.
+//
+//   cp25_quant_fp8_rows : x bf16 [M, K] -> q fp8 [M, K], s fp32 [M], x[m, k] ~= q[m, k] * s[m]
+//   cp25_gelu_quant_fp8 : the same over GELU(x) (exact erf, rounded to bf16 first as the bf16 path
+//                         leaves it: minimal_v4_dit.py:249-254), so the MLP's hidden activation is
+//                         read once and never written back in bf16
+//
+// The reference has no fp8 inference path: these are the build's own (config-5) precision option,
+// parity stated against the bf16 path in DESIGN.md §4, not a restatement of a reference kernel.
+// One to four waves per row; the row stays in registers between the amax reduction and the conversion, so
+// the kernels are one HBM read of x (2 B/element) and one write of q (1 B/element).
+#include "cp25_common.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr float kFp8Max = 448.f;  // largest finite OCP E4M3 value
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+  return v;
+}
+
+// WPR waves per row (4 / WPR rows per 256-thread block), NC chunks of 8 values per lane:
+// K = NC * WPR * 512; chunk c of wave w covers elements [(c * WPR + w) * 512 + lane * 8, +8)
+template <int WPR, int NC, bool GELU>
+__global__ void __launch_bounds__(256) quant_fp8_rows_kernel(const unsigned short* __restrict__ x,
+                                                             unsigned char* __restrict__ q, float* __restrict__ s,
+                                                             int64_t n_rows) {
+  constexpr int K = NC * WPR * 512;
+  __shared__ float red[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave % WPR;  // wave within its row
+  const int64_t row = (int64_t)blockIdx.x * (4 / WPR) + wave / WPR;
+  const bool live = row < n_rows;  // no early exit: the block meets at a barrier below
+  const int64_t base = row * K + (int64_t)wr * 512 + lane * 8;
+  // the row slice lives in registers as packed bf16 pairs (4 VGPRs per chunk) between the two passes
+  u32x4 v[NC];
+  float amax = 0.f;
+  if (live) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) v[c] = *reinterpret_cast<const u32x4*>(x + base + c * WPR * 512);
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        float lo = __uint_as_float(v[c][w] << 16), hi = __uint_as_float(v[c][w] & 0xffff0000u);
+        if constexpr (GELU) {
+          lo = rbf(0.5f * lo * (1.f + erff(lo * 0.70710678118654752440f)));
+          hi = rbf(0.5f * hi * (1.f + erff(hi * 0.70710678118654752440f)));
+          v[c][w] = (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xffff0000u);
+        }
+        amax = fmaxf(amax, fmaxf(fabsf(lo), fabsf(hi)));
+      }
+  }
+  amax = wave_max(amax);
+  if constexpr (WPR > 1) {
+    if (lane == 0) red[wave] = amax;
+    __syncthreads();
+    const int w0 = wave - wr;
+#pragma unroll
+    for (int j = 0; j < WPR; ++j) amax = fmaxf(amax, red[w0 + j]);
+  }
+  if (!live) return;
+  const float inv = amax > 0.f ? kFp8Max / amax : 0.f;
+  if (lane == 0 && wr == 0) s[row] = amax / kFp8Max;
+  unsigned char* qr = q + base;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    u32x2 o;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float f[4];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const unsigned w = v[c][2 * h + e];
+        f[2 * e] = fminf(fmaxf(__uint_as_float(w << 16) * inv, -kFp8Max), kFp8Max);
+        f[2 * e + 1] = fminf(fmaxf(__uint_as_float(w & 0xffff0000u) * inv, -kFp8Max), kFp8Max);
+      }
+      int w = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+      w = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], w, true);
+      o[h] = (unsigned)w;
+    }
+    *reinterpret_cast<u32x2*>(qr + c * WPR * 512) = o;
+  }
+}
+
+template <int WPR, int NC, bool GELU>
+void launch_rows(const unsigned short* x, unsigned char* q, float* s, int64_t n_rows, hipStream_t stream) {
+  hipLaunchKernelGGL((quant_fp8_rows_kernel<WPR, NC, GELU>), dim3((unsigned)cdiv(n_rows, 4 / WPR)), dim3(256), 0,
+                     stream, x, q, s, n_rows);
+}
+
+template <bool GELU>
+int launch_quant(const void* x, void* q, float* s, int64_t n_rows, int64_t k, hipStream_t stream) {
+  if (!x || !q || !s || n_rows <= 0) return CP25_ERR_INVAL;
+  const auto* xp = (const unsigned short*)x;
+  auto* qp = (unsigned char*)q;
+  switch (k) {
+    case 512: launch_rows<1, 1, GELU>(xp, qp, s, n_rows, stream); break;
+    case 1024: launch_rows<1, 2, GELU>(xp, qp, s, n_rows, stream); break;
+    case 1536: launch_rows<1, 3, GELU>(xp, qp, s, n_rows, stream); break;
+    case 2048: launch_rows<1, 4, GELU>(xp, qp, s, n_rows, stream); break;
+    case 3072: launch_rows<2, 3, GELU>(xp, qp, s, n_rows, stream); break;
+    case 4096: launch_rows<2, 4, GELU>(xp, qp, s, n_rows, stream); break;
+    case 5120: launch_rows<2, 5, GELU>(xp, qp, s, n_rows, stream); break;
+    case 6144: launch_rows<4, 3, GELU>(xp, qp, s, n_rows, stream); break;
+    case 8192: launch_rows<4, 4, GELU>(xp, qp, s, n_rows, stream); break;
+    case 20480: launch_rows<4, 10, GELU>(xp, qp, s, n_rows, stream); break;
+    default: return CP25_ERR_INVAL;
+  }
+  CP25_LAUNCH_CHECK();
+  return CP25_OK;
+}
+
+}  // namespace
+
+extern "C" int cp25_quant_fp8_rows(const void* x, void* q, float* scale, int64_t n_rows, int64_t k,
+                                   hipStream_t stream) {
+  return launch_quant<false>(x, q, scale, n_rows, k, stream);
+}
+
+extern "C" int cp25_gelu_quant_fp8(const void* x, void* q, float* scale, int64_t n_rows, int64_t k,
+                                   hipStream_t stream) {
+  return launch_quant<true>(x, q, scale, n_rows, k, stream);
+}

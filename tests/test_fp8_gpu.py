@@ -1,0 +1,113 @@
+"""fp8 linear layers (config 5's "fp8 MFMA" option): row quantisation kernels and the DiT's fp8 path.
+
+The reference has no fp8 inference path, so nothing here is pinned to a reference output:
+  * cp25_quant_fp8_rows / cp25_gelu_quant_fp8 are checked BIT-EXACT against the same definition in
+    torch (scale = max|row| / 448 in fp32, q = e4m3fn(clamp(x * (448 / max|row|))), RNE), the GELU
+    variant on top of cp25_gelu's bf16 output (itself checked against the reference's GELU in
+    test_dit_ops_gpu.py);
+  * one fp8 projection vs fp32 math over the dequantised operands (q * s)(w8 * ws)^T: rel-L2 <= 4e-3
+    (fp32 accumulation, one bf16 output rounding) -- checks the scale orientation end to end;
+  * a DiT forward with fp8 block GEMMs vs the bf16-path oracle: rel-L2 <= 6e-2 (stated precision cost
+    of e4m3's 3 mantissa bits: ~3.7e-2 per GEMM on random operands; measured value printed).
+"""
+import dataclasses
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from cosmos_predict2 import _native as N
+
+pytestmark = pytest.mark.gpu
+
+F8 = torch.float8_e4m3fn
+FMAX = 448.0
+
+
+def quant_ref(x: torch.Tensor):
+    xf = x.float()
+    amax = xf.abs().amax(dim=1, keepdim=True)
+    inv = torch.where(amax > 0, torch.tensor(FMAX, device=x.device) / amax, torch.zeros_like(amax))
+    q = (xf * inv).clamp(-FMAX, FMAX).to(F8)
+    # tensor / tensor: IEEE division (torch turns `/ python_scalar` into a multiply by the reciprocal)
+    return q, amax / torch.full_like(amax, FMAX)
+
+
+@pytest.mark.parametrize("M,K", [(37, 512), (5, 2048), (33, 5120), (9, 8192), (3, 20480), (64, 3072)])
+@pytest.mark.parametrize("gelu", [False, True])
+def test_quant_rows_bit_exact(device, M, K, gelu):
+    g = torch.Generator().manual_seed(M * 7 + K)
+    x = (torch.randn(M, K, generator=g) * torch.logspace(-3, 2, M).unsqueeze(1)).to(device, torch.bfloat16)
+    x[1] = 0  # all-zero row: q = 0, scale 0
+    q, s = N.quant_fp8_rows(x, gelu=gelu)
+    xr = x.clone()
+    if gelu:
+        N.gelu_(xr)
+    qr, sr = quant_ref(xr)
+    assert q.dtype == F8 and s.shape == (M, 1)
+    assert torch.equal(s, sr)
+    assert torch.equal(q.view(torch.uint8), qr.view(torch.uint8))
+    if gelu:  # the input is left untouched
+        assert not torch.equal(xr, x)
+
+
+def test_quant_rows_rejects_bad_shapes(device):
+    with pytest.raises(ValueError):
+        N.quant_fp8_rows(torch.zeros(4, 1000, device=device, dtype=torch.bfloat16))
+    with pytest.raises(ValueError):
+        N.quant_fp8_rows(torch.zeros(4, 2048, device=device, dtype=torch.float32))
+
+
+def test_fp8_linear_matches_dequantised_math(device):
+    from cosmos_predict2.dit import MinimalV1LVGDiT
+    from cosmos_predict2.net_config import tiny_dit
+
+    net = MinimalV1LVGDiT(tiny_dit(), device=device)
+    net.set_linear_precision("fp8")
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(1000, 2048, generator=g).to(device, torch.bfloat16)
+    w = (torch.randn(512, 2048, generator=g) * 0.02).to(device, torch.bfloat16)
+    for gelu in (False, True):
+        y = net._linear(x.clone(), w, f"w{gelu}", gelu_in=gelu)
+        q, s = N.quant_fp8_rows(x, gelu=gelu)
+        w8, ws = net._fp8_weight(f"w{gelu}", w)
+        ref = (q.float() * s) @ (w8.float() * ws.t()).t()
+        e = ((y.float() - ref).norm() / ref.norm()).item()
+        assert e <= 4e-3, e
+        # and the fp8 GEMM stays close to the bf16 one (the precision cost itself)
+        xb = x.clone()
+        if gelu:
+            N.gelu_(xb)
+        e_bf = ((y.float() - F.linear(xb, w).float()).norm() / F.linear(xb, w).float().norm()).item()
+        assert e_bf <= 6e-2, e_bf
+
+
+def test_dit_forward_fp8_vs_oracle(device):
+    from cosmos_predict2.dit import MinimalV1LVGDiT, init_state_dict
+    from cosmos_predict2.net_config import tiny_dit
+    from oracle import dit as odit
+
+    cfg = tiny_dit(num_blocks=2)
+    sd = {"net." + k: v for k, v in init_state_dict(cfg, seed=0, zero_adaln_out=False).items()}
+    g = torch.Generator().manual_seed(0)
+    T, H, W = 3, 16, 16
+    x = torch.randn(1, 16, T, H, W, generator=g)
+    mask = torch.zeros(1, 1, T, H, W)
+    mask[:, :, :1] = 1
+    t = torch.tensor([[0.1, 877.0, 877.0]])
+    ctx = torch.randn(1, 512, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
+    ref = odit.dit_forward(dataclasses.asdict(cfg), sd, x, t, ctx, mask)
+    net = MinimalV1LVGDiT(cfg, device=device)
+    net.load_state_dict(sd)
+    args = (x.to(device).to(torch.bfloat16), t.to(device), ctx.to(device))
+    out_bf = net(*args, condition_video_input_mask_B_C_T_H_W=mask.to(device)).cpu()
+    net.set_linear_precision("fp8")
+    out8 = net(*args, condition_video_input_mask_B_C_T_H_W=mask.to(device)).cpu()
+    e_bf = ((out_bf - ref).norm() / ref.norm()).item()
+    e8 = ((out8 - ref).norm() / ref.norm()).item()
+    print(f"dit forward rel-L2 vs oracle: bf16 {e_bf:.3e}, fp8 {e8:.3e}")
+    assert torch.isfinite(out8).all()
+    assert e8 <= 6e-2, e8
+    assert e8 > e_bf  # the fp8 path really ran
+    net.set_linear_precision("bf16")
+    assert torch.equal(net(*args, condition_video_input_mask_B_C_T_H_W=mask.to(device)).cpu(), out_bf)
