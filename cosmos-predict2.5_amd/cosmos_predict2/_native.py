@@ -56,6 +56,7 @@ SIGNATURES = {
     "cp25_attn_workspace_bytes": [_I, _I, _I, _I],
     "cp25_attn_plan": [_I, _I, _I, _I, _I],
     "cp25_ln_mod": [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _P, _P, _I64, _I, _I, _I64, _I64, _F, _P],
+    "cp25_ln_mod_fp8": [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _P, _P, _P, _I64, _I, _I, _I64, _I64, _F, _P],
     "cp25_final_ln_mod": [_P, _P, _P, _I64, _I64, _P, _P, _I64, _I64, _P, _I64, _I, _I, _I64, _I64, _F, _P],
     "cp25_head_rmsnorm_rope": [_P, _I64, _I64, _I, _I, _I, _P, _P, _P, _P, _I64, _F, _P],
     "cp25_copy_rows": [_P, _I64, _P, _I64, _I64, _I64, _P],
@@ -195,12 +196,25 @@ def _check_mask(frame_mask: torch.Tensor, *, n_tok: int, tok0: int, hw: int) -> 
 def ln_mod(x: torch.Tensor, shift: torch.Tensor, scale: torch.Tensor, *, n_tok: int, B: int, tok0: int, hw: int,
            x_st: int, x_sb: int, y: Optional[torch.Tensor] = None, gate: Optional[torch.Tensor] = None,
            x_out: Optional[torch.Tensor] = None, h_out: Optional[torch.Tensor] = None,
-           eps: float = 1e-6) -> torch.Tensor:
+           eps: float = 1e-6, fp8: bool = False):
     """h = LN(x [+ gate*y]) * (1 + scale) + shift over token-major [n_tok, B, D] bf16 rows.
-    shift/scale/gate are bf16 views [B, T, D] (strides (sb, st, 1), shared by all three)."""
+    shift/scale/gate are bf16 views [B, T, D] (strides (sb, st, 1), shared by all three).
+    fp8=True returns h as the row-scaled fp8 GEMM operand (q [n_tok*B, D] float8_e4m3fn, scale
+    [n_tok*B, 1] fp32) instead (cp25_ln_mod_fp8)."""
     lib = load_library()
     D = shift.shape[-1]
     _check_frames(shift, n_tok=n_tok, B=B, tok0=tok0, hw=hw)
+    if shift.stride() != scale.stride() or (gate is not None and gate.stride() != shift.stride()):
+        raise ValueError("shift/scale/gate must share strides")
+    if fp8:
+        q = torch.empty((n_tok * B, D), dtype=torch.float8_e4m3fn, device=x.device)
+        s = torch.empty((n_tok * B, 1), dtype=torch.float32, device=x.device)
+        rc = lib.cp25_ln_mod_fp8(
+            _ptr(x), x_st, x_sb, _ptr(y), _ptr(gate), _ptr(shift), _ptr(scale), shift.stride(0), shift.stride(1),
+            _ptr(x_out), _ptr(q), _ptr(s), n_tok, B, D, tok0, hw, eps, _stream(x.device),
+        )
+        _check("cp25_ln_mod_fp8", rc)
+        return q, s
     if h_out is None:
         h_out = torch.empty((n_tok, B, D), dtype=torch.bfloat16, device=x.device)
     if shift.stride() != scale.stride() or (gate is not None and gate.stride() != shift.stride()):

@@ -179,6 +179,11 @@ class Geometry:
         return self.T * self.Hp * self.Wp
 
 
+def _rows(h, m: int):
+    """[m, D] rows of an LN-mod output: a bf16 [n, B, D] tensor, or an fp8 (q, scale) pair as is."""
+    return h if isinstance(h, tuple) else h.view(m, -1)
+
+
 class MinimalV1LVGDiT:
     """Inference-only DiT with the reference's state-dict layout; weights live in HBM as bf16."""
 
@@ -223,14 +228,18 @@ class MinimalV1LVGDiT:
             self._fp8_w[key] = ent
         return ent
 
-    def _linear(self, x: torch.Tensor, w: torch.Tensor, key: str, gelu_in: bool = False) -> torch.Tensor:
-        """y = x w^T for a block projection (x [M, K] bf16 contiguous). bf16: hipBLASLt bf16 GEMM (GELU,
-        if asked, applied in place to x first). fp8: row-quantised x (GELU fused) times the fp8 weight."""
-        if self.linear_precision == "bf16":
+    def _linear(self, x, w: torch.Tensor, key: str, gelu_in: bool = False) -> torch.Tensor:
+        """y = x w^T for a block projection (x [M, K] bf16 contiguous, or an fp8 operand pair (q, scale)
+        that cp25_ln_mod_fp8 already produced). bf16: hipBLASLt bf16 GEMM (GELU, if asked, applied in
+        place to x first). fp8: row-quantised x (GELU fused) times the fp8 weight."""
+        if isinstance(x, tuple):
+            q, s = x
+        elif self.linear_precision == "bf16":
             if gelu_in:
                 N.gelu_(x)
             return F.linear(x, w)
-        q, s = N.quant_fp8_rows(x, gelu=gelu_in)
+        else:
+            q, s = N.quant_fp8_rows(x, gelu=gelu_in)
         w8, ws = self._fp8_weight(key, w)
         return torch._scaled_mm(q, w8.t(), scale_a=s, scale_b=ws, out_dtype=BF16)
 
@@ -507,10 +516,12 @@ class MinimalV1LVGDiT:
             m = mods[i, j]
             return m[..., :D], m[..., D:2 * D], m[..., 2 * D:]
 
+        # fp8: each LN-mod emits its h straight as the next GEMM's fp8 operand (q, scale)
         common = dict(n_tok=n, B=B, tok0=geo.tok0, hw=geo.hw)
+        lnk = dict(common, fp8=self.linear_precision == "fp8")
         sh, sc, _ = mod(0, 0)
         x = x_in
-        h = N.ln_mod(x, sh, sc, x_st=x_in.stride(0), x_sb=0 if Bx == 1 else x_in.stride(1), **common)
+        h = N.ln_mod(x, sh, sc, x_st=x_in.stride(0), x_sb=0 if Bx == 1 else x_in.stride(1), **lnk)
         y = None
         gate_prev = None
         scale_attn = hd ** -0.5
@@ -522,7 +533,7 @@ class MinimalV1LVGDiT:
             if self.attn_events is not None:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             if cp is None or cp_size == 1:
-                qkv = self._linear(h.view(n * B, D), self.w_qkv[i], f"qkv.{i}")  # [n*B, 3D]
+                qkv = self._linear(_rows(h, n * B), self.w_qkv[i], f"qkv.{i}")  # [n*B, 3D]
                 N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=0,
                                     weight=p[pre + "self_attn.q_norm.weight"], cos=cos, sin=sin)
                 N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=D,
@@ -551,10 +562,10 @@ class MinimalV1LVGDiT:
                 x_st, x_sb = x_in.stride(0), (0 if Bx == 1 else x_in.stride(1))
             else:
                 x_st, x_sb = B * D, D
-            h = N.ln_mod(x, sh, sc, x_st=x_st, x_sb=x_sb, y=y, gate=g_sa, x_out=x_new, **common)
+            h = N.ln_mod(x, sh, sc, x_st=x_st, x_sb=x_sb, y=y, gate=g_sa, x_out=x_new, **lnk)
             x = x_new
             # ---- cross attention
-            qc = self._linear(h.view(n * B, D), p[pre + "cross_attn.q_proj.weight"], pre + "cross_attn.q_proj")
+            qc = self._linear(_rows(h, n * B), p[pre + "cross_attn.q_proj.weight"], pre + "cross_attn.q_proj")
             N.head_rmsnorm_rope(qc, n_rows=n * B, B=B, H=H, head_off=0, weight=p[pre + "cross_attn.q_norm.weight"])
             o = torch.empty((n, B, D), dtype=BF16, device=self.device)
             self._cross_attention(qc.view(n, B, H, hd), ctx.k[i], ctx.v[i], o.view(n, B, H, hd), geo, scale_attn,
@@ -563,17 +574,17 @@ class MinimalV1LVGDiT:
             _, _, g_ca = mod(i, 1)
             sh, sc, _ = mod(i, 2)
             x_new = torch.empty((n, B, D), dtype=BF16, device=self.device)
-            h = N.ln_mod(x, sh, sc, x_st=B * D, x_sb=D, y=y, gate=g_ca, x_out=x_new, **common)
+            h = N.ln_mod(x, sh, sc, x_st=B * D, x_sb=D, y=y, gate=g_ca, x_out=x_new, **lnk)
             x = x_new
             # ---- MLP
-            u = self._linear(h.view(n * B, D), p[pre + "mlp.layer1.weight"], pre + "mlp.layer1")
+            u = self._linear(_rows(h, n * B), p[pre + "mlp.layer1.weight"], pre + "mlp.layer1")
             y = self._linear(u, p[pre + "mlp.layer2.weight"], pre + "mlp.layer2", gelu_in=True)
             del u
             _, _, gate_prev = mod(i, 2)
             if i + 1 < cfg.num_blocks:
                 sh, sc, _ = mod(i + 1, 0)
                 x_new = torch.empty((n, B, D), dtype=BF16, device=self.device)
-                h = N.ln_mod(x, sh, sc, x_st=B * D, x_sb=D, y=y, gate=gate_prev, x_out=x_new, **common)
+                h = N.ln_mod(x, sh, sc, x_st=B * D, x_sb=D, y=y, gate=gate_prev, x_out=x_new, **lnk)
                 x = x_new
             if cp is None or cp_size == 1:
                 yield i
@@ -613,7 +624,7 @@ class MinimalV1LVGDiT:
         p = self.sd
         pre = f"blocks.{i}."
         D, H, hd = cfg.model_channels, cfg.num_heads, cfg.head_dim
-        qkv = self._linear(h.view(n * B, D), self.w_qkv[i], f"qkv.{i}")  # [n*B, 3D]
+        qkv = self._linear(_rows(h, n * B), self.w_qkv[i], f"qkv.{i}")  # [n*B, 3D]
         N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=D, weight=p[pre + "self_attn.k_norm.weight"],
                             cos=cos, sin=sin)
         kv = torch.empty((n * B, 2 * D), dtype=BF16, device=self.device)

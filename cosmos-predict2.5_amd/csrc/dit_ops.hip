@@ -25,14 +25,18 @@
 namespace {
 
 // ---------------------------------------------------------------- LayerNorm + modulate
-template <int NC>  // NC = D / 512 chunks of 8 bf16 per lane
+// FP8: h is emitted as the row-scaled fp8 operand of the next (fp8) GEMM instead of bf16: h8_out
+// [rows, D] OCP E4M3 and h_scale [rows] = max|h_row| / 448, the same definition as cp25_quant_fp8_rows
+// applied to the bf16 h (fp8_ops.hip), without the bf16 h round trip through HBM
+template <int NC, bool FP8 = false>  // NC = D / 512 chunks of 8 bf16 per lane
 __global__ void __launch_bounds__(256) ln_mod_kernel(
     const unsigned short* __restrict__ x, int64_t x_st, int64_t x_sb,
     const unsigned short* __restrict__ y,  // optional residual branch output [tok, B, D]
     const unsigned short* __restrict__ gate, const unsigned short* __restrict__ shift,
     const unsigned short* __restrict__ scale, int64_t mod_sb, int64_t mod_st,
     unsigned short* __restrict__ x_out, unsigned short* __restrict__ h_out, int64_t n_rows, int B,
-    int64_t tok0, int64_t hw, float eps) {
+    int64_t tok0, int64_t hw, float eps, unsigned char* __restrict__ h8_out = nullptr,
+    float* __restrict__ h_scale = nullptr) {
   constexpr int D = NC * 512;
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -97,8 +101,32 @@ __global__ void __launch_bounds__(256) ln_mod_kernel(
       const float one_p = rbf(1.f + bf2f(sc[e]));           // (1 + scale)
       const float prod = rbf(ln * one_p);
       o[e] = f2bf(prod + bf2f(sh[e]));                      // + shift
+      if constexpr (FP8) v[c * 8 + e] = bf2f(o[e]);
     }
-    *reinterpret_cast<u16x8*>(h_out + row * D + off) = o;
+    if constexpr (!FP8) *reinterpret_cast<u16x8*>(h_out + row * D + off) = o;
+  }
+  if constexpr (FP8) {
+    float amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < NC * 8; ++i) amax = fmaxf(amax, fabsf(v[i]));
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) amax = fmaxf(amax, __shfl_xor(amax, m));
+    const float inv = amax > 0.f ? 448.f / amax : 0.f;
+    if (lane == 0) h_scale[row] = amax / 448.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      u32x2 o8;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        float f[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) f[e] = fminf(fmaxf(v[c * 8 + 4 * hh + e] * inv, -448.f), 448.f);
+        int w = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+        w = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], w, true);
+        o8[hh] = (unsigned)w;
+      }
+      *reinterpret_cast<u32x2*>(h8_out + row * D + (c * 64 + lane) * 8) = o8;
+    }
   }
 }
 
@@ -304,11 +332,14 @@ __global__ void __launch_bounds__(256) cfg_velocity_kernel(const float* __restri
 }  // namespace
 
 // ============================================================================ C ABI
-extern "C" int cp25_ln_mod(const void* x, int64_t x_st, int64_t x_sb, const void* y, const void* gate,
-                           const void* shift, const void* scale, int64_t mod_sb, int64_t mod_st, void* x_out,
-                           void* h_out, int64_t n_tok, int B, int D, int64_t tok0, int64_t hw, float eps,
-                           hipStream_t stream) {
-  if (n_tok <= 0 || B <= 0 || hw <= 0 || !x || !shift || !scale || !h_out) return CP25_ERR_INVAL;
+namespace {
+template <bool FP8>
+int launch_ln_mod(const void* x, int64_t x_st, int64_t x_sb, const void* y, const void* gate, const void* shift,
+                  const void* scale, int64_t mod_sb, int64_t mod_st, void* x_out, void* h_out, void* h8_out,
+                  float* h_scale, int64_t n_tok, int B, int D, int64_t tok0, int64_t hw, float eps,
+                  hipStream_t stream) {
+  if (n_tok <= 0 || B <= 0 || hw <= 0 || !x || !shift || !scale) return CP25_ERR_INVAL;
+  if (FP8 ? (!h8_out || !h_scale) : !h_out) return CP25_ERR_INVAL;
   if (y != nullptr && (gate == nullptr || x_out == nullptr)) return CP25_ERR_INVAL;
   const int64_t rows = n_tok * B;
   const dim3 grid((unsigned)cdiv(rows, 4));
@@ -319,7 +350,8 @@ extern "C" int cp25_ln_mod(const void* x, int64_t x_st, int64_t x_sb, const void
   auto* SC = (const unsigned short*)scale;
   auto* XO = (unsigned short*)x_out;
   auto* HO = (unsigned short*)h_out;
-#define LNM(NC) hipLaunchKernelGGL(ln_mod_kernel<NC>, grid, dim3(256), 0, stream, X, x_st, x_sb, Y, G, SH, SC, mod_sb, mod_st, XO, HO, rows, B, tok0, hw, eps)
+  auto* H8 = (unsigned char*)h8_out;
+#define LNM(NC) hipLaunchKernelGGL((ln_mod_kernel<NC, FP8>), grid, dim3(256), 0, stream, X, x_st, x_sb, Y, G, SH, SC, mod_sb, mod_st, XO, HO, rows, B, tok0, hw, eps, H8, h_scale)
   switch (D) {
     case 512: LNM(1); break;
     case 1024: LNM(2); break;
@@ -331,6 +363,23 @@ extern "C" int cp25_ln_mod(const void* x, int64_t x_st, int64_t x_sb, const void
 #undef LNM
   CP25_LAUNCH_CHECK();
   return CP25_OK;
+}
+}  // namespace
+
+extern "C" int cp25_ln_mod(const void* x, int64_t x_st, int64_t x_sb, const void* y, const void* gate,
+                           const void* shift, const void* scale, int64_t mod_sb, int64_t mod_st, void* x_out,
+                           void* h_out, int64_t n_tok, int B, int D, int64_t tok0, int64_t hw, float eps,
+                           hipStream_t stream) {
+  return launch_ln_mod<false>(x, x_st, x_sb, y, gate, shift, scale, mod_sb, mod_st, x_out, h_out, nullptr, nullptr,
+                              n_tok, B, D, tok0, hw, eps, stream);
+}
+
+extern "C" int cp25_ln_mod_fp8(const void* x, int64_t x_st, int64_t x_sb, const void* y, const void* gate,
+                               const void* shift, const void* scale, int64_t mod_sb, int64_t mod_st, void* x_out,
+                               void* h8_out, float* h_scale, int64_t n_tok, int B, int D, int64_t tok0, int64_t hw,
+                               float eps, hipStream_t stream) {
+  return launch_ln_mod<true>(x, x_st, x_sb, y, gate, shift, scale, mod_sb, mod_st, x_out, nullptr, h8_out, h_scale,
+                             n_tok, B, D, tok0, hw, eps, stream);
 }
 
 extern "C" int cp25_final_ln_mod(const void* x, const void* y, const void* gate, int64_t gmod_sb, int64_t gmod_st,

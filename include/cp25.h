@@ -85,6 +85,13 @@ int cp25_ln_mod(const void* x, int64_t x_st, int64_t x_sb, const void* y, const 
                 const void* scale, int64_t mod_sb, int64_t mod_st, void* x_out, void* h_out, int64_t n_tok, int B,
                 int D, int64_t tok0, int64_t hw, float eps, hipStream_t stream);
 
+/* cp25_ln_mod with h emitted as the fp8 operand of the next GEMM (config 5's fp8 option): h8_out
+ * [n_tok * B, D] OCP E4M3 and h_scale [n_tok * B] fp32, exactly cp25_quant_fp8_rows applied to the bf16 h
+ * cp25_ln_mod would write (which is not written). Same replaced reference code as cp25_ln_mod. */
+int cp25_ln_mod_fp8(const void* x, int64_t x_st, int64_t x_sb, const void* y, const void* gate, const void* shift,
+                    const void* scale, int64_t mod_sb, int64_t mod_st, void* x_out, void* h8_out, float* h_scale,
+                    int64_t n_tok, int B, int D, int64_t tok0, int64_t hw, float eps, hipStream_t stream);
+
 /* Final layer prologue under the reference's fp32 autocast: [x' = x + gate*y (bf16)], then
  * out = LayerNorm_fp32(x') * (1 + scale) + shift in fp32 (shift/scale fp32).
  * Replaces: FinalLayer.forward, minimal_v4_dit.py:974-991 (and the last block's MLP residual :1246). */

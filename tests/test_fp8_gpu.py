@@ -7,6 +7,7 @@ The reference has no fp8 inference path, so nothing here is pinned to a referenc
     test_dit_ops_gpu.py);
   * one fp8 projection vs fp32 math over the dequantised operands (q * s)(w8 * ws)^T: rel-L2 <= 4e-3
     (fp32 accumulation, one bf16 output rounding) -- checks the scale orientation end to end;
+  * cp25_ln_mod_fp8 (LN-mod emitting the fp8 operand) bit-exact vs quant_fp8_rows(cp25_ln_mod);
   * a DiT forward with fp8 block GEMMs vs the bf16-path oracle: rel-L2 <= 6e-2 (stated precision cost
     of e4m3's 3 mantissa bits: ~3.7e-2 per GEMM on random operands; measured value printed).
 """
@@ -111,3 +112,26 @@ def test_dit_forward_fp8_vs_oracle(device):
     assert e8 > e_bf  # the fp8 path really ran
     net.set_linear_precision("bf16")
     assert torch.equal(net(*args, condition_video_input_mask_B_C_T_H_W=mask.to(device)).cpu(), out_bf)
+
+
+@pytest.mark.parametrize("D,with_res", [(2048, True), (512, False), (5120, True)])
+def test_ln_mod_fp8_equals_quantised_ln_mod(device, D, with_res):
+    """cp25_ln_mod_fp8 == cp25_quant_fp8_rows(cp25_ln_mod(...)) bit for bit, x_out unchanged."""
+    n, B, T, hw = 70, 2, 3, 32
+    g = torch.Generator().manual_seed(D)
+    x = torch.randn(n, B, D, generator=g).to(device, torch.bfloat16)
+    y = torch.randn(n, B, D, generator=g).to(device, torch.bfloat16) if with_res else None
+    mods = (torch.randn(B, T, 3 * D, generator=g) * 0.5).to(device, torch.bfloat16)
+    sh, sc, gt = mods[..., :D], mods[..., D:2 * D], mods[..., 2 * D:]
+    kw = dict(n_tok=n, B=B, tok0=5, hw=hw, x_st=B * D, x_sb=D)
+    if with_res:
+        kw.update(y=y, gate=gt)
+    xo1 = torch.empty_like(x) if with_res else None
+    xo2 = torch.empty_like(x) if with_res else None
+    h = N.ln_mod(x, sh, sc, x_out=xo1, **kw)
+    q, s = N.ln_mod(x, sh, sc, x_out=xo2, fp8=True, **kw)
+    qr, sr = N.quant_fp8_rows(h.view(n * B, D))
+    assert torch.equal(s, sr)
+    assert torch.equal(q.view(torch.uint8), qr.view(torch.uint8))
+    if with_res:
+        assert torch.equal(xo1, xo2)
