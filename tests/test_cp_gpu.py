@@ -11,6 +11,8 @@ match the single-rank run (guidance 0, 2 Karras steps = 3 evals x CFG).
 * the production path against the default CP = 1 (one B = 2 pass, library split plan): GEMMs of
   batch 1 vs 2 and split vs unsplit attention round differently (~1 bf16 ulp per GEMM output,
   ~2e-3 per forward), amplified over 3 evaluations: rel-L2 <= 1.5e-2.
+* the fp8 option through the same lanes: activation scales are per token row, so a token shard
+  quantises exactly as the whole sequence does and CP = 2 must again match CP = 1 bit for bit.
 """
 import os
 import socket
@@ -55,7 +57,7 @@ def _run(model, gt, cc, cu, shape, dev):
                                 guidance=0.0, seed=0, num_steps=2).cpu()
 
 
-def _worker(rank, world, port, q, split_env):
+def _worker(rank, world, port, q, split_env, precision="bf16"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if split_env:
         os.environ["CP25_ATTN_SPLIT"] = split_env
@@ -67,6 +69,7 @@ def _worker(rank, world, port, q, split_env):
         cfg, scfg, sd, gt, cc, cu, shape = _case()
         m = Video2WorldModelRectifiedFlow(cfg, scfg, device=dev)
         m.load_state_dict(sd)
+        m.net.set_linear_precision(precision)
         m.set_context_parallel_group(dist.group.WORLD)
         out = _run(m, gt, cc, cu, shape, dev)
         q.put((rank, out.numpy()))  # by value: a shared-memory fd dies with this process
@@ -74,8 +77,8 @@ def _worker(rank, world, port, q, split_env):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("split_env,tol", [("1", 0.0), ("", 1.5e-2)])
-def test_cp2_matches_cp1(device, monkeypatch, split_env, tol):
+@pytest.mark.parametrize("split_env,tol,precision", [("1", 0.0, "bf16"), ("", 1.5e-2, "bf16"), ("1", 0.0, "fp8")])
+def test_cp2_matches_cp1(device, monkeypatch, split_env, tol, precision):
     from cosmos_predict2.model import Video2WorldModelRectifiedFlow
 
     if split_env:
@@ -85,6 +88,7 @@ def test_cp2_matches_cp1(device, monkeypatch, split_env, tol):
     cfg, scfg, sd, gt, cc, cu, shape = _case()
     m = Video2WorldModelRectifiedFlow(cfg, scfg, device=device)
     m.load_state_dict(sd)
+    m.net.set_linear_precision(precision)
     m.net.force_lanes = bool(split_env)
     ref = _run(m, gt, cc, cu, shape, device)
     del m
@@ -92,7 +96,7 @@ def test_cp2_matches_cp1(device, monkeypatch, split_env, tol):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q, split_env)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q, split_env, precision)) for r in range(2)]
     for p in ps:
         p.start()
     res = {r: torch.from_numpy(a) for r, a in (q.get(timeout=100) for _ in ps)}
@@ -101,5 +105,5 @@ def test_cp2_matches_cp1(device, monkeypatch, split_env, tol):
     assert all(p.exitcode == 0 for p in ps)
     assert torch.equal(res[0], res[1])  # every rank ends with the full gathered latent
     err = ((res[0] - ref).norm() / ref.norm()).item()
-    print(f"CP=2 vs CP=1 sampler rel-L2 (CP25_ATTN_SPLIT={split_env or 'plan'}): {err:.3e}")
+    print(f"CP=2 vs CP=1 sampler rel-L2 (CP25_ATTN_SPLIT={split_env or 'plan'}, {precision}): {err:.3e}")
     assert err <= tol, err
