@@ -191,7 +191,8 @@ int cp25_softmax_rows(const float* s, int64_t rows, int cols, int64_t ld_s, floa
  * fp8 kernel via torch._scaled_mm). Per row m of x [n_rows, k] bf16 (contiguous, k in {512, 1024, 1536,
  * 2048, 3072, 4096, 5120, 6144, 8192, 20480}): scale[m] = max|x[m, :]| / 448 and q[m, :] = fp8_e4m3(x[m, :] * 448 / max|x[m, :]|)
  * (OCP E4M3, round to nearest even, saturated), so x ~= q * scale; an all-zero row gives q = 0, scale 0.
- * cp25_gelu_quant_fp8 quantises GELU(x) (exact erf, rounded to bf16 first, as cp25_gelu leaves it).
+ * cp25_gelu_quant_fp8 quantises GELU(x) rounded to bf16 (Abramowitz-Stegun 7.1.26 erfc: within ~1 bf16 ulp
+ * of cp25_gelu's exact-erf value, far below the fp8 rounding).
  * Replaces: the bf16 operand of nn.Linear in Attention (minimal_v4_dit.py:400-432) and GPT2FeedForward
  * (:227-254, whose GELU it fuses); the reference itself has no fp8 inference path. */
 int cp25_quant_fp8_rows(const void* x, void* q, float* scale, int64_t n_rows, int64_t k, hipStream_t stream);

@@ -1,10 +1,10 @@
 """fp8 linear layers (config 5's "fp8 MFMA" option): row quantisation kernels and the DiT's fp8 path.
 
 The reference has no fp8 inference path, so nothing here is pinned to a reference output:
-  * cp25_quant_fp8_rows / cp25_gelu_quant_fp8 are checked BIT-EXACT against the same definition in
-    torch (scale = max|row| / 448 in fp32, q = e4m3fn(clamp(x * (448 / max|row|))), RNE), the GELU
-    variant on top of cp25_gelu's bf16 output (itself checked against the reference's GELU in
-    test_dit_ops_gpu.py);
+  * cp25_quant_fp8_rows is checked BIT-EXACT against the same definition in torch (scale = max|row| /
+    448 in fp32, q = e4m3fn(clamp(x * (448 / max|row|))), RNE); cp25_gelu_quant_fp8 (fast erfc GELU)
+    against that definition over cp25_gelu's exact-erf output: scales within a bf16 ulp, every code
+    within one e4m3 step, >= 97 % of codes identical;
   * one fp8 projection vs fp32 math over the dequantised operands (q * s)(w8 * ws)^T: rel-L2 <= 4e-3
     (fp32 accumulation, one bf16 output rounding) -- checks the scale orientation end to end;
   * cp25_ln_mod_fp8 (LN-mod emitting the fp8 operand) bit-exact vs quant_fp8_rows(cp25_ln_mod);
@@ -46,10 +46,19 @@ def test_quant_rows_bit_exact(device, M, K, gelu):
         N.gelu_(xr)
     qr, sr = quant_ref(xr)
     assert q.dtype == F8 and s.shape == (M, 1)
-    assert torch.equal(s, sr)
-    assert torch.equal(q.view(torch.uint8), qr.view(torch.uint8))
-    if gelu:  # the input is left untouched
-        assert not torch.equal(xr, x)
+    if not gelu:
+        assert torch.equal(s, sr)
+        assert torch.equal(q.view(torch.uint8), qr.view(torch.uint8))
+        return
+    # GELU variant: its fast erfc GELU is within ~1 bf16 ulp of cp25_gelu's exact one, so the row max
+    # (scale) may move by a bf16 ulp and a few codes by one fp8 step
+    assert torch.allclose(s, sr, rtol=2 ** -7, atol=0)
+    d = q.float() * s - qr.float() * sr
+    step = (qr.float().abs() * sr).clamp_min(1e-30) * 2.0 ** -3 + sr * 2.0 ** -9  # one e4m3 step (+ subnormal floor)
+    assert (d.abs() <= step * 1.01).all()
+    same = (q.view(torch.uint8) == qr.view(torch.uint8)).float().mean().item()
+    assert same >= 0.97, same
+    assert not torch.equal(xr, x)  # the input is left untouched
 
 
 def test_quant_rows_rejects_bad_shapes(device):
