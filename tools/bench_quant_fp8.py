@@ -11,6 +11,8 @@ import torch  # noqa: E402
 
 from cosmos_predict2 import _native as N  # noqa: E402
 
+if len(sys.argv) > 2 and sys.argv[1] == "--lib":  # lab build of libcp25.so (same-box A/B)
+    N._LIB_PATH = sys.argv[2]
 dev = torch.device("cuda:0")
 for M, K, gelu in [(218240, 8192, True), (218240, 2048, False), (9600, 8192, True), (9600, 2048, False)]:
     x = torch.randn(M, K, device=dev).to(torch.bfloat16)
@@ -25,6 +27,6 @@ for M, K, gelu in [(218240, 8192, True), (218240, 2048, False), (9600, 8192, Tru
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / it
-    print(json.dumps({"M": M, "K": K, "gelu": gelu, "ms": ms, "GB_s": 3.0 * M * K / ms / 1e6}), flush=True)
+    print(json.dumps({"lib": os.path.basename(N.library_path()), "M": M, "K": K, "gelu": gelu, "ms": ms, "GB_s": 3.0 * M * K / ms / 1e6}), flush=True)
     del x
     torch.cuda.empty_cache()
