@@ -53,12 +53,15 @@ SIGNATURES = {
                             _P, ctypes.c_size_t, _P],
     "cp25_attn_fwd_bounded": [_P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, c_int64_p, _F, _F,
                               _F, _I, _P, ctypes.c_size_t, _P],
+    "cp25_attn_fwd_prescaled": [_P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, c_int64_p, _F,
+                                _F, _I, _P, ctypes.c_size_t, _P],
     "cp25_attn_workspace_bytes": [_I, _I, _I, _I],
     "cp25_attn_plan": [_I, _I, _I, _I, _I],
     "cp25_ln_mod": [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _P, _P, _I64, _I, _I, _I64, _I64, _F, _P],
     "cp25_ln_mod_fp8": [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _P, _P, _P, _I64, _I, _I, _I64, _I64, _F, _P],
     "cp25_final_ln_mod": [_P, _P, _P, _I64, _I64, _P, _P, _I64, _I64, _P, _I64, _I, _I, _I64, _I64, _F, _P],
     "cp25_head_rmsnorm_rope": [_P, _I64, _I64, _I, _I, _I, _P, _P, _P, _P, _I64, _F, _P],
+    "cp25_head_rmsnorm_rope_scaled": [_P, _I64, _I64, _I, _I, _I, _P, _P, _P, _P, _I64, _F, _F, _P],
     "cp25_copy_rows": [_P, _I64, _P, _I64, _I64, _I64, _P],
     "cp25_gelu": [_P, _I64, _P],
     "cp25_quant_fp8_rows": [_P, _P, _P, _I64, _I64, _P],
@@ -139,12 +142,14 @@ def attn_plan(B: int, H: int, Lq: int, Lk: int, D: int = 128) -> int:
 
 def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[torch.Tensor] = None,
              softmax_scale: Optional[float] = None, n_split: Optional[int] = None,
-             norm_bounds: Optional[Tuple[float, float]] = None) -> torch.Tensor:
+             norm_bounds: Optional[Tuple[float, float]] = None, prescaled: bool = False) -> torch.Tensor:
     """softmax(q k^T * scale) v for q [B, Lq, H, 128], k/v [B, Lk, H, 128] (bf16, any strides with
     a contiguous head dim). Returns [B, Lq, H, 128] bf16. n_split: key-range split (None = the
     library's plan for this shape; the fp32 partials live in a caching-allocator workspace).
     norm_bounds: (max |q|, max |k|) upper bounds over all rows, enabling the bounded-shift softmax
-    where they are small enough (cp25_attn_fwd_bounded; None = online max only)."""
+    where they are small enough (cp25_attn_fwd_bounded; None = online max only).
+    prescaled=True: q rows already carry scale * log2(e) (head_rmsnorm_rope(out_scale=...)), norm_bounds
+    are those of the scaled q and of k with product <= 60 (cp25_attn_fwd_prescaled; softmax_scale unused)."""
     lib = load_library()
     if q.dtype != torch.bfloat16 or k.dtype != torch.bfloat16 or v.dtype != torch.bfloat16:
         raise ValueError("attn_fwd expects bf16 q/k/v (attention() recasts to bf16 first)")
@@ -166,6 +171,14 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
     qb, kb = (0.0, 0.0) if norm_bounds is None else (float(norm_bounds[0]), float(norm_bounds[1]))
     if not (qb >= 0.0 and kb >= 0.0):
         raise ValueError(f"norm_bounds must be >= 0, got {norm_bounds}")
+    strides = [_i64x3((t.stride(0), t.stride(1), t.stride(2))) for t in (q, k, v, out)]
+    if prescaled:
+        if qb * kb > 60.0 or qb <= 0.0 or kb <= 0.0:
+            raise ValueError(f"prescaled attention needs norm bounds with product <= 60, got {norm_bounds}")
+        rc = lib.cp25_attn_fwd_prescaled(_ptr(q), _ptr(k), _ptr(v), _ptr(out), B, H, Lq, Lk, D, *strides, qb, kb,
+                                         int(n_split), _ptr(ws), ws_bytes, _stream(q.device))
+        _check("cp25_attn_fwd_prescaled", rc)
+        return out
     rc = lib.cp25_attn_fwd_bounded(
         _ptr(q), _ptr(k), _ptr(v), _ptr(out), B, H, Lq, Lk, D,
         _i64x3((q.stride(0), q.stride(1), q.stride(2))),
@@ -249,11 +262,12 @@ def final_ln_mod(x: torch.Tensor, shift: torch.Tensor, scale: torch.Tensor, *, n
 
 def head_rmsnorm_rope(buf: torch.Tensor, *, n_rows: int, B: int, H: int, head_off: int, weight: torch.Tensor,
                       cos: Optional[torch.Tensor] = None, sin: Optional[torch.Tensor] = None,
-                      out2: Optional[torch.Tensor] = None, out2_stride: int = 0, eps: float = 1e-6) -> None:
+                      out2: Optional[torch.Tensor] = None, out2_stride: int = 0, eps: float = 1e-6,
+                      out_scale: float = 1.0) -> None:
     lib = load_library()
-    rc = lib.cp25_head_rmsnorm_rope(
+    rc = lib.cp25_head_rmsnorm_rope_scaled(
         _ptr(buf), buf.stride(-2) if buf.dim() >= 2 else buf.shape[-1], n_rows, B, H, head_off, _ptr(weight),
-        _ptr(cos), _ptr(sin), _ptr(out2), out2_stride, eps, _stream(buf.device),
+        _ptr(cos), _ptr(sin), _ptr(out2), out2_stride, eps, out_scale, _stream(buf.device),
     )
     _check("cp25_head_rmsnorm_rope", rc)
 

@@ -217,6 +217,16 @@ class MinimalV1LVGDiT:
         self.linear_precision = precision
         self._fp8_w = {}
 
+    def _self_attn_mode(self, i: int, hd: int):
+        """(q out_scale, attn_fwd kwargs) of block i's self-attention. bf16: the reference's rounding of
+        q. fp8 option: q leaves the RMSNorm/RoPE kernel scaled by hd^-0.5 * log2(e) and the attention
+        runs without its per-score multiply (cp25_attn_fwd_prescaled) when the norm bound allows."""
+        qb, kb = self.attn_bounds[i]
+        c = hd ** -0.5 * 1.4426950408889634
+        if self.linear_precision == "fp8" and qb * c * kb <= 60.0:
+            return c, dict(norm_bounds=(qb * c, kb), prescaled=True)
+        return 1.0, dict(softmax_scale=hd ** -0.5, norm_bounds=(qb, kb))
+
     def _fp8_weight(self, key: str, w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         ent = self._fp8_w.get(key)
         if ent is None:
@@ -534,8 +544,9 @@ class MinimalV1LVGDiT:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             if cp is None or cp_size == 1:
                 qkv = self._linear(_rows(h, n * B), self.w_qkv[i], f"qkv.{i}")  # [n*B, 3D]
+                q_scale, attn_kw = self._self_attn_mode(i, hd)
                 N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=0,
-                                    weight=p[pre + "self_attn.q_norm.weight"], cos=cos, sin=sin)
+                                    weight=p[pre + "self_attn.q_norm.weight"], cos=cos, sin=sin, out_scale=q_scale)
                 N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=D,
                                     weight=p[pre + "self_attn.k_norm.weight"], cos=cos, sin=sin)
                 q = qkv.view(n, B, 3 * D)[:, :, :D].view(n, B, H, hd).transpose(0, 1)
@@ -543,8 +554,7 @@ class MinimalV1LVGDiT:
                 vv = qkv.view(n, B, 3 * D)[:, :, 2 * D:].view(n, B, H, hd).transpose(0, 1)
                 if ev is not None:
                     ev[0].record()
-                N.attn_fwd(q, kk, vv, out=o.view(n, B, H, hd).transpose(0, 1), softmax_scale=scale_attn,
-                           norm_bounds=self.attn_bounds[i])
+                N.attn_fwd(q, kk, vv, out=o.view(n, B, H, hd).transpose(0, 1), **attn_kw)
                 lk = kk.shape[1]
             else:
                 yield from self._cp_self_attention(i, h, o, cos, sin, n, B, cp, cp_size,
@@ -632,16 +642,16 @@ class MinimalV1LVGDiT:
         kv_all = torch.empty((cp_size * n * B, 2 * D), dtype=BF16, device=self.device)
         work = all_gather_into_async(kv_all, kv, cp)  # RCCL over xGMI
         yield i  # the other lane's block runs here (in issue order) while this gather is in flight
+        q_scale, attn_kw = self._self_attn_mode(i, hd)
         N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=0, weight=p[pre + "self_attn.q_norm.weight"],
-                            cos=cos, sin=sin)
+                            cos=cos, sin=sin, out_scale=q_scale)
         work.wait()
         if e0 is not None:
             e0.record()
         kc, vc = kv_chunk_views(kv_all, cp_size * n, B, H, hd)
         q = qkv.view(n, B, 3 * D)[:, :, :D].view(n, B, H, hd).transpose(0, 1)
         # the library's key-range split plan: B = 1 launches at CP = 8 leave a ragged last round
-        N.attn_fwd(q, kc, vc, out=o.view(n, B, H, hd).transpose(0, 1), softmax_scale=hd ** -0.5,
-                   norm_bounds=self.attn_bounds[i])
+        N.attn_fwd(q, kc, vc, out=o.view(n, B, H, hd).transpose(0, 1), **attn_kw)
 
     # ---------------------------------------------------------------- reference-compatible forward
     @torch.no_grad()

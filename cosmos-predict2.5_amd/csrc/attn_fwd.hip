@@ -125,8 +125,9 @@ struct AttnArgs {
 // stages V. Buffer lifetimes: K(j) and V(j) live in buffer j&1; K(t+1), V(t) are read in phases 2t
 // and 2t+1; K(t+2) is written in phase 2t over K(t) (last read in 2t-1), V(t+1) in phase 2t+1 over
 // V(t-1) (last read in 2t-1).
-// kKind 0: self-attention, 1: cross-attention (separate symbols in profiles); kFixed: bounded shift
-template <int kKind, bool kFixed>
+// kKind 0: self-attention, 1: cross-attention (separate symbols in profiles); kFixed: bounded shift;
+// kPre: q pre-scaled by scale * log2(e) and |q| |k| <= kTop (host-checked): P = exp2(S), shift 0
+template <int kKind, bool kFixed, bool kPre = false>
 __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
 
@@ -169,7 +170,9 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   float m_run = -1e30f;
   float l_run = 0.f;
   // bounded shift: m = |q_row| * kbound * scale_log2 (the host checked the cap on the norm bounds)
-  if constexpr (kFixed) {
+  if constexpr (kPre) {
+    m_run = 0.f;
+  } else if constexpr (kFixed) {
     float qq = 0.f;
 #pragma unroll
     for (int s = 0; s < 8; ++s)
@@ -297,7 +300,8 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
         bf16x8 v;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(S[kt][8 * sp + j], a.scale_log2, -m_run));
+          const float p =
+              __builtin_amdgcn_exp2f(kPre ? S[kt][8 * sp + j] : fmaf(S[kt][8 * sp + j], a.scale_log2, -m_run));
           psum += p;
           v[j] = static_cast<__bf16>(p);
         }
@@ -536,8 +540,10 @@ extern "C" void cp25_attn_probe_set(unsigned long long* probe, int t0) { g_probe
 static int attn_launch(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq, int Lk, int D,
                        const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
                        const int64_t* o_strides, float softmax_scale, float q_norm_bound, float k_norm_bound,
-                       int n_split, void* workspace, size_t ws_bytes, hipStream_t stream) {
+                       int n_split, void* workspace, size_t ws_bytes, hipStream_t stream, bool prescaled = false) {
   if (D != kD) return CP25_ERR_DTYPE;
+  if (prescaled && !(q_norm_bound > 0.f && k_norm_bound > 0.f && (double)q_norm_bound * k_norm_bound <= (double)kTop))
+    return CP25_ERR_INVAL;
   if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0) return CP25_ERR_INVAL;
   if (!q || !k || !v || !o) return CP25_ERR_INVAL;
   if (!(softmax_scale > 0.f) || !(q_norm_bound >= 0.f) || !(k_norm_bound >= 0.f) || q_norm_bound > 1e18f ||
@@ -585,8 +591,9 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
 #endif
   const int64_t nwg = (int64_t)a.nqb * B * H * n_split;
   if (nwg > 0x7fffffff) return CP25_ERR_INVAL;
-  auto kernel = Lk <= 4096 ? (fixed ? attn_fwd_d128<1, true> : attn_fwd_d128<1, false>)
-                           : (fixed ? attn_fwd_d128<0, true> : attn_fwd_d128<0, false>);
+  auto kernel = prescaled ? (Lk <= 4096 ? attn_fwd_d128<1, true, true> : attn_fwd_d128<0, true, true>)
+                : Lk <= 4096 ? (fixed ? attn_fwd_d128<1, true> : attn_fwd_d128<1, false>)
+                             : (fixed ? attn_fwd_d128<0, true> : attn_fwd_d128<0, false>);
   hipLaunchKernelGGL(kernel, dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
   CP25_LAUNCH_CHECK();
   if (n_split > 1) {
@@ -632,4 +639,13 @@ extern "C" int cp25_attn_fwd_bounded(const void* q, const void* k, const void* v
                                      size_t ws_bytes, hipStream_t stream) {
   return attn_launch(q, k, v, o, B, H, Lq, Lk, D, q_strides, k_strides, v_strides, o_strides, softmax_scale,
                      q_norm_bound, k_norm_bound, n_split, workspace, ws_bytes, stream);
+}
+
+extern "C" int cp25_attn_fwd_prescaled(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq,
+                                       int Lk, int D, const int64_t* q_strides, const int64_t* k_strides,
+                                       const int64_t* v_strides, const int64_t* o_strides, float q_norm_bound,
+                                       float k_norm_bound, int n_split, void* workspace, size_t ws_bytes,
+                                       hipStream_t stream) {
+  return attn_launch(q, k, v, o, B, H, Lq, Lk, D, q_strides, k_strides, v_strides, o_strides, 0.6931471805599453f,
+                     q_norm_bound, k_norm_bound, n_split, workspace, ws_bytes, stream, true);
 }

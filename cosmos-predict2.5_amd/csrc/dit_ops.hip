@@ -195,7 +195,7 @@ __global__ void __launch_bounds__(256) final_ln_mod_kernel(
 __global__ void __launch_bounds__(256) head_rmsnorm_rope_kernel(
     unsigned short* __restrict__ buf, int64_t row_stride, int64_t n_rows, int B, int H, int head_off,
     const unsigned short* __restrict__ w, const float* __restrict__ cosb, const float* __restrict__ sinb,
-    unsigned short* __restrict__ out2, int64_t out2_stride, float eps) {
+    unsigned short* __restrict__ out2, int64_t out2_stride, float eps, float out_scale) {
   const int64_t item = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);  // (row, head)
   const int li = threadIdx.x & 15;
   if (item >= n_rows * H) return;
@@ -233,7 +233,7 @@ __global__ void __launch_bounds__(256) head_rmsnorm_rope_kernel(
   }
   u16x8 o;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e]);
+  for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e] * out_scale);  // out_scale 1: exact, the reference's rounding
   *reinterpret_cast<u16x8*>(p) = o;
   if (out2 != nullptr) *reinterpret_cast<u16x8*>(out2 + row * out2_stride + h * 128 + li * 8) = o;
 }
@@ -409,12 +409,20 @@ extern "C" int cp25_final_ln_mod(const void* x, const void* y, const void* gate,
 extern "C" int cp25_head_rmsnorm_rope(void* buf, int64_t row_stride, int64_t n_rows, int B, int H, int head_off,
                                       const void* weight, const float* cos_tab, const float* sin_tab, void* out2,
                                       int64_t out2_stride, float eps, hipStream_t stream) {
+  return cp25_head_rmsnorm_rope_scaled(buf, row_stride, n_rows, B, H, head_off, weight, cos_tab, sin_tab, out2,
+                                       out2_stride, eps, 1.f, stream);
+}
+
+extern "C" int cp25_head_rmsnorm_rope_scaled(void* buf, int64_t row_stride, int64_t n_rows, int B, int H,
+                                             int head_off, const void* weight, const float* cos_tab,
+                                             const float* sin_tab, void* out2, int64_t out2_stride, float eps,
+                                             float out_scale, hipStream_t stream) {
   if (!buf || !weight || n_rows <= 0 || H <= 0 || B <= 0) return CP25_ERR_INVAL;
   if ((row_stride % 8) || (head_off % 8) || ((cos_tab == nullptr) != (sin_tab == nullptr))) return CP25_ERR_INVAL;
   const int64_t items = n_rows * H;
   hipLaunchKernelGGL(head_rmsnorm_rope_kernel, dim3((unsigned)cdiv(items, 16)), dim3(256), 0, stream,
                      (unsigned short*)buf, row_stride, n_rows, B, H, head_off, (const unsigned short*)weight, cos_tab,
-                     sin_tab, (unsigned short*)out2, out2_stride, eps);
+                     sin_tab, (unsigned short*)out2, out2_stride, eps, out_scale);
   CP25_LAUNCH_CHECK();
   return CP25_OK;
 }

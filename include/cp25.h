@@ -64,6 +64,17 @@ int cp25_attn_fwd_bounded(const void* q, const void* k, const void* v, void* o, 
                           const int64_t* o_strides, float softmax_scale, float q_norm_bound, float k_norm_bound,
                           int n_split, void* workspace, size_t ws_bytes, hipStream_t stream);
 
+/* Bounded-shift attention over a PRE-SCALED q (rows already multiplied by softmax_scale * log2(e), e.g.
+ * by cp25_head_rmsnorm_rope_scaled): P = exp2(q k^T) with no per-score multiply and no shift. Requires
+ * q_norm_bound * k_norm_bound <= 60 (bounds of |q_row| as scaled and of |k_row|), which keeps every
+ * term in [2^-60, 2^60]; CP25_ERR_INVAL otherwise (the caller then runs cp25_attn_fwd_bounded on an
+ * unscaled q). Rounds q * scale to bf16 instead of q: the config-5 fp8 option's attention.
+ * Replaces the same reference code as cp25_attn_fwd_bounded. */
+int cp25_attn_fwd_prescaled(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq, int Lk, int D,
+                            const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
+                            const int64_t* o_strides, float q_norm_bound, float k_norm_bound, int n_split,
+                            void* workspace, size_t ws_bytes, hipStream_t stream);
+
 /* Bytes of workspace cp25_attn_fwd_split / _bounded need (0 for n_split <= 1). */
 size_t cp25_attn_workspace_bytes(int B, int H, int Lq, int n_split);
 
@@ -108,6 +119,13 @@ int cp25_final_ln_mod(const void* x, const void* y, const void* gate, int64_t gm
 int cp25_head_rmsnorm_rope(void* buf, int64_t row_stride, int64_t n_rows, int B, int H, int head_off,
                            const void* weight, const float* cos_tab, const float* sin_tab, void* out2,
                            int64_t out2_stride, float eps, hipStream_t stream);
+
+/* cp25_head_rmsnorm_rope with the result multiplied by out_scale (fp32) before its bf16 rounding: the
+ * fp8 option's q = q * softmax_scale * log2(e), so its attention needs no per-score multiply
+ * (cp25_attn_fwd_prescaled). out_scale = 1 is cp25_head_rmsnorm_rope exactly. */
+int cp25_head_rmsnorm_rope_scaled(void* buf, int64_t row_stride, int64_t n_rows, int B, int H, int head_off,
+                                  const void* weight, const float* cos_tab, const float* sin_tab, void* out2,
+                                  int64_t out2_stride, float eps, float out_scale, hipStream_t stream);
 
 /* dst[r, 0:width] = src[r, 0:width] for bf16 rows (K/V export before the CP all-gather). */
 int cp25_copy_rows(const void* src, int64_t src_stride, void* dst, int64_t dst_stride, int64_t n_rows, int64_t width,

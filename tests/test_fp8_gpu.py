@@ -144,3 +144,30 @@ def test_ln_mod_fp8_equals_quantised_ln_mod(device, D, with_res):
     assert torch.equal(q.view(torch.uint8), qr.view(torch.uint8))
     if with_res:
         assert torch.equal(xo1, xo2)
+
+
+@pytest.mark.parametrize("Lq,Lk,n_split", [(300, 1000, None), (513, 9000, 3), (256, 64, None)])
+def test_prescaled_attention_vs_fp32(device, Lq, Lk, n_split):
+    """cp25_attn_fwd_prescaled (the fp8 option's self-attention): q arrives multiplied by
+    scale * log2(e) (rounded to bf16 there), P = exp2(q k^T); vs fp32 softmax(q k^T / sqrt(d)) v on the
+    unscaled q: rel-L2 <= 4e-3 (the P/O bf16 floor plus the q * c rounding)."""
+    B, H, D = 2, 3, 128
+    g = torch.Generator().manual_seed(Lq + Lk)
+
+    def rms_rows(L):
+        x = torch.randn(B, L, H, D, generator=g)
+        return x / x.pow(2).mean(-1, keepdim=True).sqrt()  # |row| = sqrt(128), like the DiT's q/k norm
+
+    q, k = rms_rows(Lq), rms_rows(Lk)
+    v = torch.randn(B, Lk, H, D, generator=g)
+    qb = kb = D ** 0.5 * 1.02
+    c = D ** -0.5 * 1.4426950408889634
+    qd, kd, vd = q.to(device, torch.bfloat16), k.to(device, torch.bfloat16), v.to(device, torch.bfloat16)
+    ref = torch.softmax(torch.einsum("blhd,bmhd->bhlm", qd.float(), kd.float()) * D ** -0.5, -1)
+    ref = torch.einsum("bhlm,bmhd->blhd", ref, vd.float())
+    qs = (qd.float() * c).to(torch.bfloat16)
+    out = N.attn_fwd(qs, kd, vd, norm_bounds=(qb * c, kb), prescaled=True, n_split=n_split)
+    e = ((out.float() - ref).norm() / ref.norm()).item()
+    assert e <= 4e-3, e
+    with pytest.raises(ValueError):  # bound product over 60: refused (the caller keeps the unscaled path)
+        N.attn_fwd(qs, kd, vd, norm_bounds=(8.0, 8.0), prescaled=True)
