@@ -1,15 +1,21 @@
 """Benchmark: frames/sec of Predict2.5-2B Image2World at 704x1280 x 121 frames, 35 UniPC steps.
 
-One step = one full Image2World video through the product API (Video2WorldInference.generate_vid2world):
-VAE encode of the conditioning frame, 35 Karras UniPC steps = 36 DiT evaluations x CFG 2 (cond and
-uncond batched, B = 2) on the 2B network at latent [16, 31, 88, 160] (L = 109 120 tokens), VAE decode
-of all 31 latent frames to 121 pixel frames. Synthetic data: seeded random weights with the 2B shapes,
-a random conditioning image, N(0, 1) text embeddings [1, 512, 100352]. bf16 compute.
+The workload is one Image2World video through the product model (Video2WorldModelRectifiedFlow):
+VAE encode of the conditioning frame, sampler setup (noise, schedule, per-prompt text context),
+35 Karras UniPC steps = 36 sampler evaluations, VAE decode of all 31 latent frames to 121 frames.
+
+One bench *step* = one full-geometry sampler evaluation (SamplingRun.step(): patchify + frame
+replacement, the CFG-batched B = 2 DiT forward on the 2B net at latent [16, 31, 88, 160],
+L = 109 120 tokens, GT-frame velocity replacement + CFG, fused UniPC update). The encode, the setup
+and the 121-frame decode are timed once each in the same run (barrier + synchronize around each);
+  value = frames / (t_encode + t_setup + evals_per_video * t_step + t_decode)
+i.e. whole-video frames/s. Synthetic data: seeded random weights with the 2B shapes, a random
+conditioning image, N(0, 1) text embeddings [1, 512, 100352]. bf16 compute.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
 N > 1 (torchrun, one rank per GPU, RCCL): the video's token sequence is sharded context-parallel over
-the N ranks (K/V all-gather over xGMI); all ranks work on the same video (strong scaling).
-Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement").
+the N ranks (K/V all-gather over xGMI), the decode is banded over the ranks; all ranks work on the
+same video (strong scaling). Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement").
 """
 from __future__ import annotations
 
@@ -35,8 +41,8 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1", "attn_pmc_r1e", "SUMMARY.json
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1, help="timed videos")
-    ap.add_argument("--warmup", type=int, default=0, help="untimed videos before timing")
+    ap.add_argument("--steps", type=int, default=10, help="timed sampler evaluations")
+    ap.add_argument("--warmup", type=int, default=2, help="untimed sampler evaluations before timing")
     ap.add_argument("--num-steps", type=int, default=35, help="UniPC steps (35 = the metric)")
     ap.add_argument("--frames", type=int, default=121)
     ap.add_argument("--model", default="2B/post-trained",
@@ -54,7 +60,7 @@ def parse():
 
 
 def _heartbeat(rank: int, period: float = 30.0) -> None:
-    """Progress line on stderr every `period` s (a video takes minutes; keeps watchdogs informed)."""
+    """Progress line on stderr every `period` s (keeps watchdogs informed)."""
     t0 = time.time()
 
     def beat():
@@ -65,6 +71,30 @@ def _heartbeat(rank: int, period: float = 30.0) -> None:
     threading.Thread(target=beat, daemon=True).start()
 
 
+class _Timer:
+    """Barrier + device synchronize on both sides; max over ranks."""
+
+    def __init__(self, world: int, dev):
+        self.world, self.dev = world, dev
+
+    def _sync(self):
+        torch.cuda.synchronize(self.dev)
+        if self.world > 1:
+            dist.barrier()
+
+    def __call__(self, fn):
+        self._sync()
+        t0 = time.perf_counter()
+        out = fn()
+        self._sync()
+        el = time.perf_counter() - t0
+        if self.world > 1:
+            tt = torch.tensor([el], device=self.dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = tt.item()
+        return out, el
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -72,6 +102,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}: launch N>1 with torch.distributed.run")
+    if a.steps < 1:
+        raise SystemExit("--steps must be >= 1")
     _heartbeat(rank)
     dev = torch.device("cuda", 0 if a.share_device else local)
     torch.cuda.set_device(dev)
@@ -81,7 +113,7 @@ def main():
         else:
             dist.init_process_group(a.backend)
 
-    from cosmos_predict2.pipeline import Video2WorldInference
+    from cosmos_predict2.pipeline import DEFAULT_NEGATIVE_PROMPT, Video2WorldInference
     from cosmos_predict2 import _native
 
     _native.load_library()
@@ -89,42 +121,55 @@ def main():
     state_t = 1 + (a.frames - 1) // 4
     pipe = Video2WorldInference(a.model, context_parallel_size=world, device=dev, state_t=state_t,
                                 linear_precision=a.linear_precision)
-    karras = pipe.model.config.use_kerras_sigma_at_inference
-    frames = pipe.model.tokenizer.get_pixel_num_frames(state_t)
+    model = pipe.model
+    karras = model.config.use_kerras_sigma_at_inference
+    frames = model.tokenizer.get_pixel_num_frames(state_t)
     # conditioning "image": frame 0 random uint8, later frames zero (read_and_process_image layout)
     rng = np.random.RandomState(3)
     vid = torch.zeros(1, 3, frames, h, w, dtype=torch.uint8)
     vid[0, :, 0] = torch.from_numpy(rng.randint(0, 256, size=(3, h, w), dtype=np.uint8))
-    kw = dict(prompt="A robot arm pours coffee into a mug on a kitchen counter.", input_path=vid, guidance=7,
-              num_latent_conditional_frames=1, resolution=f"{h},{w}", seed=0, num_steps=a.num_steps)
+    batch = pipe._get_data_batch_input(vid, "A robot arm pours coffee into a mug on a kitchen counter.", 1,
+                                       DEFAULT_NEGATIVE_PROMPT)
+    state_shape = (model.config.state_ch, state_t, h // 8, w // 8)
+    timer = _Timer(world, dev)
 
-    # kernel-load prime (not a warmup step): one DiT evaluation + one latent frame decode
-    net = pipe.model.net
+    # ---- kernel-load prime (untimed): encode, one evaluation, a 2-latent-frame decode
     with torch.no_grad():
-        pipe.generate_vid2world(**dict(kw, num_steps=1)) if a.warmup == 0 else None
-    for _ in range(a.warmup):
-        pipe.generate_vid2world(**kw)
+        gt = model.encode_conditioning(batch["video"], 1, state_t)
+        run = model.begin_sampling(gt, batch["t5_text_embeddings"], batch["neg_t5_text_embeddings"],
+                                   state_shape=state_shape, num_conditional_frames=1, guidance=7, seed=0,
+                                   num_steps=a.num_steps)
+        run.step()
+        model.decode(run.latents()[:, :, :2])
+        del run, gt
 
-    net.attn_events = []
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        video = pipe.generate_vid2world(**kw)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = tt.item()
-    assert video.shape[2] == frames and torch.isfinite(video).all()
+        # ---- per-video pieces timed once
+        gt, t_enc = timer(lambda: model.encode_conditioning(batch["video"], 1, state_t))
+        run, t_setup = timer(lambda: model.begin_sampling(
+            gt, batch["t5_text_embeddings"], batch["neg_t5_text_embeddings"], state_shape=state_shape,
+            num_conditional_frames=1, guidance=7, seed=0, num_steps=a.num_steps))
+        evals = run.num_evals
 
-    # dominant kernel: self-attention flash kernel, HIP events around every launch in the timed region
-    ev = net.attn_events
-    net.attn_events = None
+        def advance(k):
+            for _ in range(k):
+                if run.done:  # more evaluations than one trajectory: start it over (same work per step)
+                    run.restart()
+                run.step()
+
+        advance(a.warmup)
+        net = model.net
+        net.attn_events = []
+        _, t_steps = timer(lambda: advance(a.steps))
+        ev = net.attn_events
+        net.attn_events = None
+        t_step = t_steps / a.steps
+        lat = run.latents()
+        video, t_dec = timer(lambda: model.decode(lat))
+        assert video.shape[2] == frames and torch.isfinite(video.float()).all()
+
+    video_s = t_enc + t_setup + evals * t_step + t_dec
+    # dominant kernel: self-attention flash kernel, HIP events on its launch stream around every
+    # launch in the timed steps
     attn_ms = [e0.elapsed_time(e1) for e0, e1, _ in ev]
     attn_flop = ev[0][2] if ev else 0.0
     attn_avg_s = (sum(attn_ms) / len(attn_ms)) / 1e3 if attn_ms else float("nan")
@@ -135,28 +180,28 @@ def main():
         sys.path.insert(0, ROOT)
         from oracle.cpu_baseline import dit_block_sample
 
-        cpu = dit_block_sample(L=state_t * (h // 16) * (w // 16), threads=a.cpu_threads)
+        cpu = dit_block_sample(L=state_t * (h // 16) * (w // 16), threads=a.cpu_threads,
+                               forwards=2 * evals, frames=frames)
 
     if rank == 0:
-        ms = elapsed / a.steps * 1e3
         valid = (a.num_steps == 35 and a.frames == 121 and (h, w) == (704, 1280) and a.model == "2B/post-trained"
                  and a.linear_precision == "bf16")
-        # HBM bytes per self-attention launch from the committed rocprofv3 PMC passes of this kernel
-        # at this shape (tools/pmc_attn.sh, FETCH_SIZE x2 gfx950 correction + WRITE_SIZE); only the
-        # CP = 1 metric shape was measured, so other shapes report null
+        # HBM bytes per self-attention launch: a static prior from the committed rocprofv3 PMC passes of
+        # this kernel at this shape (tools/pmc_attn.sh; FETCH_SIZE x2 gfx950 correction + WRITE_SIZE),
+        # not collected in this run; only the CP = 1 metric shape was measured, other shapes report null
         traffic, traffic_src = None, None
         if world == 1 and valid and os.path.exists(PMC_SUMMARY):
             with open(PMC_SUMMARY) as f:
                 traffic = json.load(f).get("traffic_bytes_per_launch")
-            traffic_src = os.path.relpath(PMC_SUMMARY, ROOT)
+            traffic_src = "static prior: " + os.path.relpath(PMC_SUMMARY, ROOT) + " (rocprofv3 PMC, not this run)"
         line = {
             "metric": METRIC,
-            "value": frames * a.steps / elapsed,
+            "value": frames / video_s,
             "unit": "frames/s",
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": ms,
+            "ms_per_step": t_step * 1e3,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -164,9 +209,14 @@ def main():
             "data": "synthetic: seeded random 2B/VAE weights, random conditioning image, N(0,1) text embeddings",
             "config": {
                 "workload": f"Predict2.5-2B Image2World {h}x{w}x{frames}f ({a.model}), {a.num_steps} "
-                            + (f"Karras UniPC steps ({a.num_steps + 1} evals" if karras else
-                               f"shift-5 UniPC steps ({a.num_steps} evals")
+                            + (f"Karras UniPC steps ({evals} evals" if karras else f"shift-5 UniPC steps ({evals} evals")
                             + f" x CFG 2, batched), VAE encode cond frame + decode {frames}f",
+                "step": "one sampler evaluation: CFG-batched (B=2) DiT forward + CFG + UniPC update",
+                "evals_per_video": evals,
+                "seconds_per_video": video_s,
+                "encode_s": t_enc,
+                "setup_s": t_setup,
+                "decode_s": t_dec,
                 "latent": [16, state_t, h // 8, w // 8],
                 "tokens": state_t * (h // 16) * (w // 16),
                 "global_batch": 1,
@@ -187,7 +237,6 @@ def main():
                 "avg_launch_ms": attn_avg_s * 1e3,
                 "flop_per_launch": attn_flop,
             },
-            "phases_last_step_s": getattr(pipe, "last_timing", None),
             "cpu_baseline": cpu and {k: cpu[k] for k in ("value", "unit", "cores", "kind", "sample")},
         }
         print(json.dumps(line), flush=True)

@@ -97,6 +97,19 @@ class Video2WorldModelRectifiedFlow:
 
     # ------------------------------------------------------------------ the sampler
     @torch.no_grad()
+    def begin_sampling(self, gt: Optional[torch.Tensor], ctx_cond: torch.Tensor, ctx_uncond: torch.Tensor, *,
+                       state_shape, num_conditional_frames: int, guidance: float, seed: int, num_steps: int,
+                       shift: float = 5.0, cfg_mode: Optional[str] = None, net_fn=None,
+                       action: Optional[torch.Tensor] = None,
+                       view_indices: Optional[torch.Tensor] = None) -> "SamplingRun":
+        """Set up one trajectory of the sampling loop (text2world_model_rectified_flow.py:556-582):
+        noise, schedule, conditioning; SamplingRun.step() then runs one loop iteration (:584-594)."""
+        return SamplingRun(self, gt, ctx_cond, ctx_uncond, state_shape=state_shape,
+                           num_conditional_frames=num_conditional_frames, guidance=guidance, seed=seed,
+                           num_steps=num_steps, shift=shift, cfg_mode=cfg_mode, net_fn=net_fn, action=action,
+                           view_indices=view_indices)
+
+    @torch.no_grad()
     def sample_latents(self, gt: Optional[torch.Tensor], ctx_cond: torch.Tensor, ctx_uncond: torch.Tensor, *,
                        state_shape, num_conditional_frames: int, guidance: float, seed: int, num_steps: int,
                        shift: float = 5.0, cfg_mode: Optional[str] = None, progress=None,
@@ -105,56 +118,15 @@ class Video2WorldModelRectifiedFlow:
         """Core loop. gt: x0 latent [1, C, T, H, W] fp32 (or None when no frame is conditioned);
         ctx_*: text embeddings [1, Lctx, proj_in]. Returns latents [1, C, T, H, W] fp32.
         net_fn(rows [n,1,72] bf16, t_B_T [2,T] fp32, geo) -> [n,2,64] replaces the DiT (tests only)."""
-        C, T, H, W = state_shape
-        dev = self.device
-        geo = Geometry(T=T, Hp=H // 2, Wp=W // 2, n_views=self.net.n_views_for(T))
-        L = geo.L
-        cp = self.cp_group
-        rank, world = (0, 1) if cp is None else (torch.distributed.get_rank(cp), torch.distributed.get_world_size(cp))
-        if L % world:
-            raise ValueError(f"token count {L} not divisible by the context-parallel size {world}")
-        geo.n_tok = L // world
-        geo.tok0 = rank * geo.n_tok
-        sl = slice(geo.tok0, geo.tok0 + geo.n_tok)
-
-        noise_full = arch_invariant_rand((1, C, T, H, W), torch.float32, dev, seed)
-        noise = to_patch_layout(noise_full[0])[sl].contiguous()
-        del noise_full
-        frame_mask = torch.zeros(T, dtype=torch.float32, device=dev)
-        if geo.T_view > 1 and num_conditional_frames > 0:
-            # the first frames of every view (multi-view FIRST_RANDOM_N, predict2_multiview/configs/vid2vid/
-            # defaults/conditioner.py:125-260; one view: video2world conditioner.py:45-143)
-            for vi in range(geo.n_views):
-                frame_mask[vi * geo.T_view: vi * geo.T_view + num_conditional_frames] = 1.0
-        gtp = None
-        if gt is not None and num_conditional_frames > 0:
-            gtp = to_patch_layout(gt[0].to(dev, torch.float32))[sl].contiguous()
-
-        ctx = None if net_fn is not None else self.net.prepare_context(torch.cat([ctx_cond, ctx_uncond], 0))
-        mode = 0 if (cfg_mode or self.config.cfg_mode) == "video2world" else 1
-
-        sched = self.sample_scheduler
-        sched.set_timesteps(num_steps, device=dev, shift=shift,
-                            use_kerras_sigma=self.config.use_kerras_sigma_at_inference)
-        x = sched.begin(noise)
-        scale = self.net_cfg.timestep_scale
-        for i, t in enumerate(sched.timesteps.cpu()):
-            rows = N.patchify(x, gtp, frame_mask, None, tok0=geo.tok0, hw=geo.hw)
-            tf = self._frame_timesteps(t, frame_mask)  # [T]
-            t_B_T = (tf[None, :] * scale).expand(2, T).contiguous()
-            if net_fn is None:
-                net_out = self.net.forward_tokens(rows.view(geo.n_tok, 1, -1), t_B_T, ctx, geo, action=action,
-                                                  view_indices=view_indices)
-            else:
-                net_out = net_fn(rows.view(geo.n_tok, 1, -1), t_B_T, geo)
-            v = N.cfg_velocity(net_out, noise, gtp, frame_mask, guidance, mode, tok0=geo.tok0, hw=geo.hw)
-            del net_out
-            sched.step_(v, t)
+        run = self.begin_sampling(gt, ctx_cond, ctx_uncond, state_shape=state_shape,
+                                  num_conditional_frames=num_conditional_frames, guidance=guidance, seed=seed,
+                                  num_steps=num_steps, shift=shift, cfg_mode=cfg_mode, net_fn=net_fn,
+                                  action=action, view_indices=view_indices)
+        while not run.done:
+            i = run.step()
             if progress is not None:
-                progress(i, len(sched.timesteps))
-        if world > 1:
-            x = cpu.gather_tokens(x, cp)
-        return from_patch_layout(x, T, H, W).unsqueeze(0)
+                progress(i, run.num_evals)
+        return run.latents()
 
     @torch.no_grad()
     def generate_samples_from_batch(self, data_batch: Dict, guidance: float = 1.5, seed: int = 1,
@@ -162,6 +134,18 @@ class Video2WorldModelRectifiedFlow:
                                     is_negative_prompt: bool = False, num_steps: int = 35, shift: float = 5.0,
                                     **kwargs) -> torch.Tensor:
         """text2world_model_rectified_flow.py:516-599 (+ the Video2World velocity_fn)."""
+        run = self.begin_sampling_from_batch(data_batch, guidance=guidance, seed=seed, state_shape=state_shape,
+                                             is_negative_prompt=is_negative_prompt, num_steps=num_steps, shift=shift)
+        while not run.done:
+            run.step()
+        return run.latents()
+
+    @torch.no_grad()
+    def begin_sampling_from_batch(self, data_batch: Dict, guidance: float = 1.5, seed: int = 1, state_shape=None,
+                                  is_negative_prompt: bool = False, num_steps: int = 35,
+                                  shift: float = 5.0) -> "SamplingRun":
+        """generate_samples_from_batch up to its loop: encode the conditioning frames (VAE), build the
+        CFG contexts, noise and schedule; returns the steppable SamplingRun."""
         video = data_batch["video"]
         if state_shape is None:
             _T, _H, _W = video.shape[-3:]
@@ -179,7 +163,7 @@ class Video2WorldModelRectifiedFlow:
             ctx_u = torch.zeros_like(ctx_c)  # TextAttr dropout (rate 0.2 > 0) zeroes the embedding
         # action-conditioned nets: the same action conditions both CFG branches (the conditioner's
         # action ReMapkey has no dropout: action/configs/action_conditioned/conditioner.py:222-233,272-275)
-        return self.sample_latents(gt, ctx_c, ctx_u, state_shape=state_shape, num_conditional_frames=n_cond,
+        return self.begin_sampling(gt, ctx_c, ctx_u, state_shape=state_shape, num_conditional_frames=n_cond,
                                    guidance=guidance, seed=seed, num_steps=num_steps, shift=shift,
                                    action=data_batch.get("action"))
 
@@ -221,3 +205,99 @@ class Video2WorldModelRectifiedFlow:
         if self.config.denoise_replace_gt_frames:
             out = (noise - gt.type_as(out)) * m + out * (1 - m)
         return out
+
+
+class SamplingRun:
+    """One sampler trajectory of Video2WorldModelRectifiedFlow, advanced one evaluation at a time.
+
+    Setup = text2world_model_rectified_flow.py:556-582 (noise, schedule, conditioning); step() = one
+    iteration of the loop at :584-594 (patchify + frame replacement, the CFG-batched DiT forward,
+    GT-frame velocity replacement + CFG, fused UniPC update); latents() = :596-599 (CP gather)."""
+
+    def __init__(self, model: "Video2WorldModelRectifiedFlow", gt, ctx_cond, ctx_uncond, *, state_shape,
+                 num_conditional_frames: int, guidance: float, seed: int, num_steps: int, shift: float = 5.0,
+                 cfg_mode: Optional[str] = None, net_fn=None, action=None, view_indices=None):
+        self.model = model
+        C, T, H, W = state_shape
+        self.state_shape = (C, T, H, W)
+        dev = model.device
+        geo = Geometry(T=T, Hp=H // 2, Wp=W // 2, n_views=model.net.n_views_for(T))
+        L = geo.L
+        cp = model.cp_group
+        rank, world = (0, 1) if cp is None else (torch.distributed.get_rank(cp), torch.distributed.get_world_size(cp))
+        if L % world:
+            raise ValueError(f"token count {L} not divisible by the context-parallel size {world}")
+        geo.n_tok = L // world
+        geo.tok0 = rank * geo.n_tok
+        sl = slice(geo.tok0, geo.tok0 + geo.n_tok)
+        self.geo, self.cp, self.world = geo, cp, world
+
+        noise_full = arch_invariant_rand((1, C, T, H, W), torch.float32, dev, seed)
+        self.noise = to_patch_layout(noise_full[0])[sl].contiguous()
+        del noise_full
+        frame_mask = torch.zeros(T, dtype=torch.float32, device=dev)
+        if geo.T_view > 1 and num_conditional_frames > 0:
+            # the first frames of every view (multi-view FIRST_RANDOM_N, predict2_multiview/configs/vid2vid/
+            # defaults/conditioner.py:125-260; one view: video2world conditioner.py:45-143)
+            for vi in range(geo.n_views):
+                frame_mask[vi * geo.T_view: vi * geo.T_view + num_conditional_frames] = 1.0
+        self.frame_mask = frame_mask
+        self.gtp = None
+        if gt is not None and num_conditional_frames > 0:
+            self.gtp = to_patch_layout(gt[0].to(dev, torch.float32))[sl].contiguous()
+
+        self.net_fn = net_fn
+        self.ctx = None if net_fn is not None else model.net.prepare_context(torch.cat([ctx_cond, ctx_uncond], 0))
+        self.mode = 0 if (cfg_mode or model.config.cfg_mode) == "video2world" else 1
+        self.guidance = guidance
+        self.action, self.view_indices = action, view_indices
+        self._sched_args = dict(num_inference_steps=num_steps, device=dev, shift=shift,
+                                use_kerras_sigma=model.config.use_kerras_sigma_at_inference)
+        self.restart()
+
+    def restart(self) -> None:
+        """Back to the first timestep from the same noise (bench: more evaluations than one trajectory)."""
+        sched = self.model.sample_scheduler
+        sched.set_timesteps(**self._sched_args)
+        self.timesteps = sched.timesteps.cpu()
+        self.x = sched.begin(self.noise)
+        self.i = 0
+
+    @property
+    def num_evals(self) -> int:
+        return len(self.timesteps)
+
+    @property
+    def done(self) -> bool:
+        return self.i >= len(self.timesteps)
+
+    @torch.no_grad()
+    def step(self) -> int:
+        """One sampler evaluation; returns its index in the schedule."""
+        if self.done:
+            raise RuntimeError("the trajectory is complete (restart() to run it again)")
+        m, geo = self.model, self.geo
+        t = self.timesteps[self.i]
+        rows = N.patchify(self.x, self.gtp, self.frame_mask, None, tok0=geo.tok0, hw=geo.hw)
+        tf = m._frame_timesteps(t, self.frame_mask)  # [T]
+        t_B_T = (tf[None, :] * m.net_cfg.timestep_scale).expand(2, geo.T).contiguous()
+        if self.net_fn is None:
+            net_out = m.net.forward_tokens(rows.view(geo.n_tok, 1, -1), t_B_T, self.ctx, geo, action=self.action,
+                                           view_indices=self.view_indices)
+        else:
+            net_out = self.net_fn(rows.view(geo.n_tok, 1, -1), t_B_T, geo)
+        v = N.cfg_velocity(net_out, self.noise, self.gtp, self.frame_mask, self.guidance, self.mode,
+                           tok0=geo.tok0, hw=geo.hw)
+        del net_out
+        m.sample_scheduler.step_(v, t)
+        self.i += 1
+        return self.i - 1
+
+    @torch.no_grad()
+    def latents(self) -> torch.Tensor:
+        """The current latent state [1, C, T, H, W] fp32 (all-gathered over the CP group)."""
+        x = self.x
+        if self.world > 1:
+            x = cpu.gather_tokens(x, self.cp)
+        _, T, H, W = self.state_shape
+        return from_patch_layout(x, T, H, W).unsqueeze(0)

@@ -78,9 +78,11 @@ def read_and_process_image(img_path: str, resolution, num_video_frames: int, res
 
 
 def process_video_frames(frames_uint8_T_H_W_C: torch.Tensor, resolution, num_video_frames: int,
-                         num_latent_conditional_frames: int = 2, resize: bool = True) -> torch.Tensor:
-    """read_and_process_video on already-decoded frames: keep the last 4(n-1)+1, pad with the last."""
-    if num_latent_conditional_frames not in (1, 2):
+                         num_latent_conditional_frames: int = 2, resize: bool = True,
+                         validate: bool = True) -> torch.Tensor:
+    """read_and_process_video on already-decoded frames: keep the last 4(n-1)+1, pad with the last.
+    validate=False: the AR loop's copy of this logic (video2world.py:657-690) accepts any n."""
+    if validate and num_latent_conditional_frames not in (1, 2):
         raise ValueError(f"num_latent_conditional_frames must be 1 or 2, but got {num_latent_conditional_frames}")
     v = frames_uint8_T_H_W_C.float().permute(3, 0, 1, 2) / 255.0  # [C, T, H, W]
     need = 4 * (num_latent_conditional_frames - 1) + 1
@@ -229,28 +231,76 @@ class Video2WorldInference:
                                            num_latent_conditional_frames: int = 1, resolution: str = "192,320",
                                            seed: int = 1, negative_prompt: str = DEFAULT_NEGATIVE_PROMPT,
                                            num_steps: int = 35, **unused) -> torch.Tensor:
-        """Sliding-window long-video generation (video2world.py:582-810): chunk i is conditioned on
-        the last `chunk_overlap` frames of chunk i-1 (re-quantised to uint8), seed + i."""
+        """Sliding-window long-video generation (video2world.py:582-810), byte-for-byte the reference's
+        window: a running uint8 input video `current_input_video` of num_output_frames frames; chunk i
+        covers frames [i*(chunk_size-overlap), +chunk_size) (zero-padded to the model's frame count),
+        is generated with seed + i and `chunk_overlap` as its num_latent_conditional_frames (the
+        reference passes the pixel overlap there, :761-765), and writes its frames from
+        [start + cond, end) back into the running video, re-quantised by truncation
+        ((v/2 + 0.5).clamp(0, 1) * 255).to(uint8) (:796-804). Output: chunk 0 whole, later chunks
+        without their first `chunk_overlap` frames (:785-793)."""
         if resolution == "none":
             h, w = VIDEO_RES_SIZE_INFO[self.model.config.resolution]["9,16"]
         else:
             h, w = (int(x) for x in resolution.split(","))
-        tok = self.model.tokenizer
-        frames = tok.get_pixel_num_frames(self.model.config.state_t)
-        if chunk_size > frames:
-            raise ValueError(f"chunk_size {chunk_size} exceeds the model's {frames} frames")
-        n_chunks = 1 + max(0, math.ceil((num_output_frames - chunk_size) / (chunk_size - chunk_overlap)))
-        cond = input_path
+        frames = self.model.tokenizer.get_pixel_num_frames(self.model.config.state_t)
+        full = self._ar_input_video(input_path, num_output_frames, num_latent_conditional_frames, (h, w))
+        step = chunk_size - chunk_overlap
+        if step <= 0:
+            raise ValueError(f"chunk_overlap {chunk_overlap} must be smaller than chunk_size {chunk_size}")
+        rem = num_output_frames - chunk_size
+        n_chunks = 1 if rem <= 0 else 1 + (rem + step - 1) // step
+        current = full.clone()
         pieces = []
         for ci in range(n_chunks):
-            nlat = num_latent_conditional_frames if ci == 0 else (1 + (chunk_overlap - 1) // 4)
-            video = self.generate_vid2world(prompt, cond, guidance, frames, nlat, f"{h},{w}", seed + ci,
+            start = ci * step
+            end = min(start + chunk_size, num_output_frames)
+            if start >= num_output_frames:
+                break
+            n = end - start
+            chunk_in = current[:, :, start:end]
+            if n < frames:
+                pad = torch.zeros(chunk_in.shape[:2] + (frames - n,) + chunk_in.shape[3:], dtype=chunk_in.dtype)
+                chunk_in = torch.cat([chunk_in, pad], dim=2)
+            n_cond = num_latent_conditional_frames if ci == 0 else chunk_overlap
+            video = self.generate_vid2world(prompt, chunk_in, guidance, frames, n_cond, resolution, seed + ci,
                                             negative_prompt, num_steps)
-            video = video[:, :, :chunk_size]
+            video = video[:, :, :n]
             pieces.append(video if ci == 0 else video[:, :, chunk_overlap:])
-            last = ((video[0, :, -chunk_overlap:] + 1) / 2 * 255).round().clamp(0, 255).to(torch.uint8).cpu()
-            nxt = torch.zeros(1, 3, frames, h, w, dtype=torch.uint8)
-            nxt[0, :, :chunk_overlap] = last
-            nxt[0, :, chunk_overlap:] = last[:, -1:]
-            cond = nxt
-        return torch.cat(pieces, 2)[:, :, :num_output_frames]
+            if ci < n_chunks - 1:
+                v8 = ((video / 2.0 + 0.5).clamp(0.0, 1.0) * 255.0).to(torch.uint8)
+                current[:, :, start + n_cond:end] = v8[:, :, n_cond:].to(current.device)
+        return torch.cat(pieces, dim=2)
+
+    @staticmethod
+    def _ar_input_video(input_path, num_output_frames: int, num_latent_conditional_frames: int,
+                        resolution) -> torch.Tensor:
+        """The AR loop's full-length uint8 input [1, 3, num_output_frames, H, W] (video2world.py:637-708):
+        zeros (no input / text2world), image as frame 0 + zeros, the last 4(n-1)+1 video frames + repeats
+        of the last, or a given uint8 tensor zero-padded in time."""
+        h, w = resolution
+        if input_path is None or num_latent_conditional_frames == 0:
+            return torch.zeros(1, 3, num_output_frames, h, w, dtype=torch.uint8)
+        if isinstance(input_path, torch.Tensor):
+            v = input_path
+            if v.shape[2] < num_output_frames:
+                pad = torch.zeros(v.shape[:2] + (num_output_frames - v.shape[2],) + v.shape[3:], dtype=v.dtype)
+                v = torch.cat([v, pad], dim=2)
+            return v
+        if not isinstance(input_path, str):
+            raise ValueError(f"Unsupported input_path type: {type(input_path)}")
+        ext = os.path.splitext(input_path)[1].lower()
+        if ext in _IMAGE_EXTENSIONS:
+            from PIL import Image
+
+            img = np.asarray(Image.open(input_path).convert("RGB"))
+            img = (torch.from_numpy(img.copy()).permute(2, 0, 1)[None].float() / 255.0 * 255.0).to(torch.uint8)
+            img = resize_input(img, resolution)
+            vid = torch.cat([img, torch.zeros_like(img).repeat(num_output_frames - 1, 1, 1, 1)], dim=0)
+            return vid.unsqueeze(0).permute(0, 2, 1, 3, 4)
+        if ext in _VIDEO_EXTENSIONS:
+            from .video_io import read_mp4
+
+            return process_video_frames(torch.from_numpy(read_mp4(input_path)), resolution, num_output_frames,
+                                        num_latent_conditional_frames, validate=False)
+        raise ValueError(f"Unsupported file extension: {ext}")
