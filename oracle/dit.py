@@ -23,6 +23,7 @@ Weights: a state dict with the reference's `net.` key layout, bf
 """
 from __future__ import annotations
 
+import contextlib
 import math
 
 import torch
@@ -31,9 +32,28 @@ import torch.nn.functional as F
 BF16 = torch.bfloat16
 F32 = torch.float32
 
+# activation dtype of the restatement: bf16 = the reference's inference arithmetic; fp32 (inside
+# `fp32_truth()`) = the same bf16-valued weights with every activation kept in fp32 (no intermediate
+# bf16 rounding), the "truth" both the bf16 reference and the HIP path are measured against
+_ACT = [BF16]
+
+
+def act_dtype() -> torch.dtype:
+    return _ACT[-1]
+
+
+@contextlib.contextmanager
+def fp32_truth():
+    _ACT.append(F32)
+    try:
+        yield
+    finally:
+        _ACT.pop()
+
 
 def _w(sd, name):
-    return sd["net." + name]
+    w = sd["net." + name]
+    return w.float() if _ACT[-1] == F32 else w
 
 
 def te_rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-6) -> torch.Tensor:
@@ -95,7 +115,7 @@ def sdpa(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, chunk: int = 4096) -
         p = torch.softmax(torch.matmul(qf, kf.transpose(-1, -2)) * (D ** -0.5), dim=-1)
         outs.append(torch.matmul(p, vf).transpose(1, 2))
     o = torch.cat(outs, dim=1)
-    return o.reshape(B, Lq, H * D).to(BF16)
+    return o.reshape(B, Lq, H * D).to(act_dtype())
 
 
 def _lin(x, w, b=None):
@@ -106,7 +126,7 @@ def action_embedding(cfg, sd, action: torch.Tensor):
     """action_conditioned_minimal_v1_lvg_dit.py: Mlp (:28-45: fc1 + bias, GELU(tanh), fc2 + bias) in
     the model dtype (bf16) on the action [B, A, d]; per chunk (:104-107) -> [B, 1, *], per latent
     frame (:257-270) -> [B, A/r, *] with a zero row prepended for latent frame 0."""
-    a = action.to(BF16)
+    a = action.to(act_dtype())
     B, A, d = a.shape
     r = cfg.get("action_per_latent_frame", 0)
     a = a.reshape(B, A // r, r * d) if r else a.reshape(B, 1, A * d)
@@ -159,7 +179,7 @@ def block_forward(cfg, sd, i, x, emb, lora, ctx, freqs, n_views: int = 1):
     sh_sa, sc_sa, g_sa = adaln(sd, p + "adaln_modulation_self_attn", emb, lora)
     sh_ca, sc_ca, g_ca = adaln(sd, p + "adaln_modulation_cross_attn", emb, lora)
     sh_ml, sc_ml, g_ml = adaln(sd, p + "adaln_modulation_mlp", emb, lora)
-    cvt = lambda t: t[:, :, None, None, :].to(BF16)  # noqa: E731
+    cvt = lambda t: t[:, :, None, None, :].to(act_dtype())  # noqa: E731
     sh_sa, sc_sa, g_sa, sh_ca, sc_ca, g_ca, sh_ml, sc_ml, g_ml = map(
         cvt, (sh_sa, sc_sa, g_sa, sh_ca, sc_ca, g_ca, sh_ml, sc_ml, g_ml)
     )
@@ -174,7 +194,7 @@ def block_forward(cfg, sd, i, x, emb, lora, ctx, freqs, n_views: int = 1):
     k = te_rmsnorm(k, _w(sd, p + "self_attn.k_norm.weight")).float()
     q = apply_rope(q, freqs)
     k = apply_rope(k, freqs)
-    o = sdpa(q.to(BF16), k.to(BF16), v.to(BF16))
+    o = sdpa(q.to(act_dtype()), k.to(act_dtype()), v.to(act_dtype()))
     o = _lin(o, _w(sd, p + "self_attn.output_proj.weight")).reshape(B, T, H, W, D)
     x = x + g_sa * o
 
@@ -209,13 +229,13 @@ def dit_forward(cfg: dict, sd: dict, x_B_C_T_H_W: torch.Tensor, timesteps_B_T: t
                 crossattn_emb: torch.Tensor, cond_mask_B_1_T_H_W: torch.Tensor,
                 padding_mask_B_1_H_W: torch.Tensor | None = None, action: torch.Tensor | None = None) -> torch.Tensor:
     """-> velocity [B, C, T, H, W] fp32 (the model applies .float(), text2world_model_rectified_flow.py:860)."""
-    x = x_B_C_T_H_W.to(BF16)
+    x = x_B_C_T_H_W.to(act_dtype())
     B, C, T, Hl, Wl = x.shape
-    x = torch.cat([x, cond_mask_B_1_T_H_W.to(BF16)], dim=1)  # minimal_v1_lvg_dit.py:46
+    x = torch.cat([x, cond_mask_B_1_T_H_W.to(act_dtype())], dim=1)  # minimal_v1_lvg_dit.py:46
     t = timesteps_B_T * cfg["timestep_scale"]
     if cfg["concat_padding_mask"]:
         pm = padding_mask_B_1_H_W if padding_mask_B_1_H_W is not None else torch.zeros(B, 1, Hl, Wl)
-        pm = F.interpolate(pm.float(), size=(Hl, Wl), mode="nearest").to(BF16)
+        pm = F.interpolate(pm.float(), size=(Hl, Wl), mode="nearest").to(act_dtype())
         x = torch.cat([x, pm[:, :, None].expand(B, 1, T, Hl, Wl)], dim=1)
     n_views = T // cfg["state_t"] if cfg.get("n_cameras_emb", 0) else 1
     if n_views > 1 or cfg.get("n_cameras_emb", 0):
@@ -224,7 +244,7 @@ def dit_forward(cfg: dict, sd: dict, x_B_C_T_H_W: torch.Tensor, timesteps_B_T: t
         ve = _w(sd, "view_embeddings.weight")[vidx]  # [V, vdim] bf16
         Tv = T // n_views
         vch = ve.t()[None, :, :, None, None, None].expand(B, ve.shape[1], n_views, Tv, Hl, Wl)
-        x = torch.cat([x.view(B, x.shape[1], n_views, Tv, Hl, Wl), vch.to(BF16)], 1).reshape(B, -1, T, Hl, Wl)
+        x = torch.cat([x.view(B, x.shape[1], n_views, Tv, Hl, Wl), vch.to(act_dtype())], 1).reshape(B, -1, T, Hl, Wl)
     ps, pt = cfg["patch_spatial"], cfg["patch_temporal"]
     Tp, Hp, Wp = T // pt, Hl // ps, Wl // ps
     # b c (t r) (h m) (w n) -> b t h w (c r m n)
@@ -234,7 +254,7 @@ def dit_forward(cfg: dict, sd: dict, x_B_C_T_H_W: torch.Tensor, timesteps_B_T: t
     # MultiCameraVideoRopePosition3DEmb (multiview_dit.py:108-130): positions restart per view
     freqs = rope_freqs(cfg, Tp // n_views, Hp, Wp).repeat(n_views, 1)
 
-    ctx = crossattn_emb.to(BF16)
+    ctx = crossattn_emb.to(act_dtype())
     if cfg["use_crossattn_projection"]:
         ctx = F.gelu(_lin(ctx, _w(sd, "crossattn_proj.0.weight"), _w(sd, "crossattn_proj.0.bias")))
 

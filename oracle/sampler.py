@@ -45,7 +45,7 @@ def denoise(cfg_dit, sd, noise, xt, t_B_T, ctx, gt, mask, cond_frame_t: float, r
         t = (tc * m_t + t_B_T * (1 - m_t)).squeeze()
         t_B_T = t.unsqueeze(0) if t.ndim == 1 else t
     fn = dit_fn or odit.dit_forward
-    out = fn(cfg_dit, sd, xt.to(torch.bfloat16), t_B_T, ctx, mask.to(torch.bfloat16)).float()
+    out = fn(cfg_dit, sd, xt.to(odit.act_dtype()), t_B_T, ctx, mask.to(odit.act_dtype())).float()
     if replace_gt:
         gv = noise - gt.type_as(out)
         out = gv * m + out * (1 - m)

@@ -1,0 +1,102 @@
+"""Full-depth parity at BASELINE config 1 geometry, measured against an fp32 truth.
+
+Config 1 (256x256x9 frames -> latent [16, 3, 32, 32], 768 tokens) at the real 2B network: all 28
+blocks, D 2048, 16 heads, crossattn_proj 100352 -> 1024, AdaLN-LoRA 256; seeded weights with the
+reference's init distributions (AdaLN output layers randomised so modulation is exercised).
+
+Three distances on identical inputs (rel-L2 of the fp32 output):
+  hip  vs truth : the MI355X path against the fp32 truth (oracle.dit.fp32_truth(): the same bf16
+                  weights, every activation in fp32);
+  ref  vs truth : the bf16 oracle (the reference's inference arithmetic, op for op) against the truth;
+  hip  vs ref   : the MI355X path against the bf16 oracle.
+The reference itself is a bf16 computation, so its own distance from the truth is the scale of any
+bf16 implementation's error: the gate is that the HIP path is no further from the truth than the bf16
+reference restatement is (times a small factor), and hip-vs-ref is bounded by the measured values.
+The reference's only numeric DiT test (CP vs non-CP, rel-L2 < 5e-3,
+_src/predict2/interactive/networks/dit_causal_test.py:200-201) is the model for a bf16-vs-bf16 bound.
+Measured values are printed (pytest -s) and recorded in DESIGN.md §4.
+"""
+import dataclasses
+
+import pytest
+import torch
+
+from cosmos_predict2.dit import MinimalV1LVGDiT, init_state_dict
+from cosmos_predict2.model import Video2WorldModelRectifiedFlow
+from cosmos_predict2.net_config import DIT_2B, SamplerConfig
+from oracle import dit as odit
+from oracle import sampler as osamp
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm()).item()
+
+
+@pytest.fixture(scope="module")
+def net2b():
+    cfg = DIT_2B
+    sd = {"net." + k: v for k, v in init_state_dict(cfg, seed=11, zero_adaln_out=False).items()}
+    return cfg, sd
+
+
+def _report(name, hip, ref, truth):
+    d = dict(hip_truth=rel(hip, truth), ref_truth=rel(ref, truth), hip_ref=rel(hip, ref))
+    print(f"{name}: hip-vs-truth {d['hip_truth']:.3e}  bf16ref-vs-truth {d['ref_truth']:.3e}  "
+          f"hip-vs-bf16ref {d['hip_ref']:.3e}")
+    return d
+
+
+def test_full_depth_2b_forward(device, net2b):
+    """One 28-block forward at config-1 geometry (cond frame t 0.1, the others mid-trajectory)."""
+    cfg, sd = net2b
+    g = torch.Generator().manual_seed(31)
+    T, H, W = 3, 32, 32
+    x = torch.randn(1, 16, T, H, W, generator=g)
+    mask = torch.zeros(1, 1, T, H, W)
+    mask[:, :, :1] = 1
+    t = torch.tensor([[0.1, 877.0, 877.0]])
+    ctx = torch.randn(1, 512, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
+    c = dataclasses.asdict(cfg)
+    ref = odit.dit_forward(c, sd, x, t, ctx, mask)
+    with odit.fp32_truth():
+        truth = odit.dit_forward(c, sd, x, t, ctx, mask)
+    net = MinimalV1LVGDiT(cfg, device=device)
+    net.load_state_dict(sd)
+    hip = net(x.to(device).to(torch.bfloat16), t.to(device), ctx.to(device),
+              condition_video_input_mask_B_C_T_H_W=mask.to(device)).cpu()
+    d = _report("28-block 2B forward (config-1 geometry)", hip, ref, truth)
+    assert torch.isfinite(hip).all()
+    # measured (MI355X, round 2): hip-truth 1.162e-2, ref-truth 1.164e-2, hip-ref 8.81e-3
+    assert d["hip_truth"] <= 1.1 * d["ref_truth"], d
+    assert d["hip_ref"] <= 1.2e-2, d
+
+
+@pytest.mark.parametrize("guidance", [0.0, 7.0])
+def test_full_depth_2b_sampler(device, net2b, guidance):
+    """Karras 2 steps (3 evaluations x CFG) of the 28-block 2B net at config-1 geometry, the metric's
+    guidance 7 and guidance 0."""
+    cfg, sd = net2b
+    T, H, W = 3, 32, 32
+    g = torch.Generator().manual_seed(71)
+    gt = torch.randn(1, 16, T, H, W, generator=g)
+    ctx_c = torch.randn(1, 512, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
+    ctx_u = torch.randn(1, 512, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
+    c = dataclasses.asdict(cfg)
+    kw = dict(num_cond=1, guidance=guidance, seed=0, num_steps=2, use_karras=True, cond_frame_t=0.1)
+    ref = osamp.generate(c, sd, gt, ctx_c, ctx_u, **kw)
+    with odit.fp32_truth():
+        truth = osamp.generate(c, sd, gt, ctx_c, ctx_u, **kw)
+    model = Video2WorldModelRectifiedFlow(cfg, SamplerConfig(use_kerras_sigma_at_inference=True,
+                                                             conditional_frame_timestep=0.1), device=device)
+    model.load_state_dict(sd)
+    hip = model.sample_latents(gt.to(device), ctx_c.to(device), ctx_u.to(device), state_shape=(16, T, H, W),
+                               num_conditional_frames=1, guidance=guidance, seed=0, num_steps=2).cpu()
+    d = _report(f"28-block 2B sampler, Karras 2 steps, g={guidance}", hip, ref, truth)
+    assert torch.isfinite(hip).all()
+    # measured (MI355X, round 2): g=0 hip-truth 1.567e-2, ref-truth 1.563e-2, hip-ref 1.274e-2;
+    # g=7 1.421e-1, 1.425e-1, 1.376e-1 (c + 7 (c - u) amplifies the per-branch bf16 error ~15x:
+    # random text contexts make c and u differ by only ~2.5 %, tools/diag_batch.py)
+    assert d["hip_truth"] <= 1.1 * d["ref_truth"], d
+    assert d["hip_ref"] <= (1.6e-2 if guidance == 0 else 1.8e-1), d
