@@ -9,7 +9,7 @@ split_inputs_cp / cat_outputs_cp / broadcast equivalents on the token axis.
 """
 from __future__ import annotations
 
-from typing import Optional
+from typing import Generator, List, Optional
 
 import torch
 import torch.distributed as dist
@@ -70,6 +70,45 @@ def all_gather_into_async(out: torch.Tensor, x: torch.Tensor, group):
     w = dist.get_world_size(group)
     return dist.all_gather_into_tensor(out.view((w * x.shape[0],) + tuple(x.shape[1:])), x.contiguous(),
                                        group=group, async_op=True)
+
+
+def run_lanes(lanes: List[Generator]) -> list:
+    """Round-robin driver of software-pipelined lanes on ONE stream (dit.forward_tokens, CP > 1).
+
+    Each lane is a generator that queues device work on the current stream, starts an asynchronous
+    collective (all_gather_into_async), yields, and on its next step waits for that collective
+    (`work.wait()`: the current stream waits for the collective's completion event) before queueing
+    the work that reads the gathered data. Driving the lanes in rotation queues lane b+1's whole
+    block between lane b's gather and lane b's wait, so the transfer overlaps that compute.
+
+    Stream / allocator invariant this relies on (and why the lanes are not on separate streams):
+      * every kernel and every work.wait() is on the one current stream, so program order is
+        stream order: no event edges between compute streams exist to mis-order or deadlock;
+      * every tensor is allocated and freed on that stream (caching-allocator pool of the current
+        stream); the only buffers another stream touches are a collective's input and output, which
+        the process group keeps alive (record_stream / stash) until the collective's stream is done;
+      * a round-1 variant ran the lanes on two streams with cross-stream events (lane 1 waiting on
+        an event lane 0 recorded after queueing its gather) and hung intermittently in device
+        synchronisation when two ranks shared one GPU over gloo. The hazard that variant had and
+        this one cannot: HIP multiplexes streams onto a few hardware queues per process
+        (GPU_MAX_HW_QUEUES = 4 here; default + 2 lanes + the gloo staging copies + RCCL's stream
+        already exceed it), and an event-wait packet at the head of a shared hardware queue blocks
+        every stream mapped behind it; with the gloo staging path doing blocking host copies inside
+        a lane, a wait queued ahead of the record it depends on (in another stream sharing the
+        queue) cannot drain. One stream has no such edge.
+    Returns each lane's return value, in lane order."""
+    live = [True] * len(lanes)
+    out = [None] * len(lanes)
+    while any(live):
+        for i, g in enumerate(lanes):
+            if not live[i]:
+                continue
+            try:
+                next(g)
+            except StopIteration as e:
+                out[i] = e.value
+                live[i] = False
+    return out
 
 
 def kv_chunk_views(kv_all_c: torch.Tensor, n_tok_total: int, B: int, Hc: int, hd: int):

@@ -23,7 +23,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _native as N
-from .context_parallel import all_gather_into_async, kv_chunk_views
+from .context_parallel import all_gather_into_async, kv_chunk_views, run_lanes
 from .net_config import DiTConfig
 
 BF16 = torch.bfloat16
@@ -495,20 +495,9 @@ class MinimalV1LVGDiT:
         for b in range(B):
             cb = ContextCache(B=1, k=[t[b:b + 1] for t in ctx.k], v=[t[b:b + 1] for t in ctx.v])
             xb = x_in[:, (0 if Bx == 1 else b):(0 if Bx == 1 else b) + 1]
-            lanes.append([self._blocks(xb, mods[:, :, b:b + 1], shift_f[b:b + 1], scale_f[b:b + 1], cb, geo, cos,
-                                       sin, cp, cp_size), None])
-        live = B
-        while live:
-            for lane in lanes:
-                if lane[0] is None:
-                    continue
-                try:
-                    next(lane[0])
-                except StopIteration as e:
-                    lane[1] = e.value
-                    lane[0] = None
-                    live -= 1
-        return torch.cat([o for _, o in lanes], dim=1)
+            lanes.append(self._blocks(xb, mods[:, :, b:b + 1], shift_f[b:b + 1], scale_f[b:b + 1], cb, geo, cos,
+                                      sin, cp, cp_size))
+        return torch.cat(run_lanes(lanes), dim=1)
 
     def _blocks(self, x_in, mods, shift_f, scale_f, ctx: ContextCache, geo: Geometry, cos, sin, cp, cp_size):
         """Generator: issues the 28 blocks + final layer for the batch entries in x_in/mods/ctx on the

@@ -461,6 +461,314 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// One wave per SIMD ("1w"): a workgroup = 4 waves = 256 query rows of one (b, h); each wave owns 64
+// rows as two 32-row q-blocks and the whole register file (launch bound 1 wave/SIMD; O and Q live in
+// the accumulator file, the softmax in the arch VGPRs). The wave is software-pipelined over 32-key
+// half tiles with a lag of two on P.V: sub-step i issues
+//     QK^T(i+1)  (16 MFMAs, K rows from LDS)   and   P.V(i-1)  (16 MFMAs, V rows from LDS, P(i-1))
+// none of which depends on this sub-step's VALU, and runs the softmax of half i (S(i), computed in
+// sub-step i-1, -> P(i)) in their issue gaps: 32 scores per lane = 32 exp + 32 fma + 32 add + 16
+// packs, 3.5 VALU per MFMA gap with one transcendental each (MI355X_MICROARCH: <= 5 fillers per
+// 32x32x16 gap hide behind the matrix pipe); there is no partner wave to arbitrate with.
+// Same MFMA fragments as attn_fwd_d128 (swapped S^T = K Q^T, O^T = V^T P^T, V^T by transposed LDS
+// reads of row-major V) and the same padded LDS rows; bounded-shift / prescaled softmax only (the
+// DiT's forms; the online-max form stays on attn_fwd_d128).
+// One loop iteration t = two sub-steps (halves 2t, 2t+1) and one barrier; it reads K(t), K(t+1),
+// V(t-1), V(t) and stages K(t+2), V(t+1) (register-staged by all four waves: loads at the top of a
+// sub-step, LDS writes at its end) into a 3-deep ring, K(j) / V(j) in slot j % 3: K(t+2) overwrites
+// K(t-1), V(t+1) overwrites V(t-2), both last read in iteration t-1.
+constexpr int kThreads1w = 256;
+
+// S^T MFMAs of attn_fwd_1w as inline asm: the scores must land in arch VGPRs (the softmax reads them
+// with VALU; the builtin puts them in the accumulator file and copies them back, 32 v_accvgpr_read per
+// half tile), with the Q operand held in the accumulator file. Hazard (MFMA D -> VALU read): every
+// consumer of these results is issued >= 4 MFMAs later (next sub-step) or behind explicit s_nops.
+__device__ __forceinline__ void mfma_s_init(f32x16& d, const bf16x8& k, const bf16x8& q) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(k), "a"(q));
+}
+__device__ __forceinline__ void mfma_s_acc(f32x16& d, const bf16x8& k, const bf16x8& q) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(k), "a"(q));
+}
+constexpr int kLds1w = 3 * kKBuf + 3 * kVBuf;  // 113664
+
+template <int kKind, bool kPre>
+__global__ void __launch_bounds__(kThreads1w, 1) attn_fwd_1w(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[kLds1w];
+
+  const int nwg = gridDim.x;
+  const int tile = xcd_remap(blockIdx.x, nwg);
+  const int qblk = tile % a.nqb, bhs = tile / a.nqb;
+  const int split = bhs % a.nsplit, bh = bhs / a.nsplit;
+  const int b = bh / a.H, h = bh % a.H;
+  const int key0 = split * a.tps * kKBlk;
+  const int Lk = min(a.Lk - key0, a.tps * kKBlk);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l31 = lane & 31;
+  const int hl = lane >> 5;
+
+  const unsigned short* qp = a.q + b * a.q_sb + h * a.q_sh;
+  const unsigned short* kp = a.k + b * a.k_sb + h * a.k_sh + (int64_t)key0 * a.k_sl;
+  const unsigned short* vp = a.v + b * a.v_sb + h * a.v_sh + (int64_t)key0 * a.v_sl;
+
+  // ---- Q fragments of the wave's two q-blocks, and each row's fixed softmax shift ----
+  bf16x8 qf[2][8];
+  float m_sh[2];
+  int q_row[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    q_row[j] = qblk * kQBlk + wave * 64 + 32 * j + l31;
+    const int qc = q_row[j] < a.Lq ? q_row[j] : a.Lq - 1;
+    const unsigned short* src = qp + (int64_t)qc * a.q_sl + 8 * hl;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) qf[j][s] = *reinterpret_cast<const bf16x8*>(src + 16 * s);
+    if constexpr (kPre) {
+      m_sh[j] = 0.f;
+    } else {
+      float qq = 0.f;
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = static_cast<float>(qf[j][s][e]);
+          qq = fmaf(x, x, qq);
+        }
+      qq = wave_swap_sum(qq);
+      m_sh[j] = fmaxf(sqrtf(qq) * a.kbound * a.scale_log2 - kTop, 0.f);
+    }
+  }
+
+  f32x16 o[4][2];
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[d][j][r] = 0.f;
+  float l_run[2] = {0.f, 0.f};
+
+  const int ntiles = (Lk + kKBlk - 1) / kKBlk;
+
+  // ---- staging: all 256 threads, 4 x 16 B of a 64-row tile each: rows tid/16 + 16 i ----
+  const int srow = tid >> 4, sch = tid & 15;
+  const int stk_off = (int)(srow * a.k_sl * 2) + sch * 16, stk_step = (int)(16 * a.k_sl * 2);
+  const int stv_off = (int)(srow * a.v_sl * 2) + sch * 16, stv_step = (int)(16 * a.v_sl * 2);
+  u32x4 st[4];
+  // tile t of K (kv = 0) or V (kv = 1); tiles past the end read as zeros (empty descriptor)
+  auto load_tile = [&](int kv, int t) __attribute__((always_inline)) {
+    const int64_t sl = kv ? a.v_sl : a.k_sl;
+    const unsigned short* base = kv ? vp : kp;
+    // rows of tile t inside [0, Lk) (0 past the end), branch-free: the descriptor's range check
+    // zero-fills the rest
+    const int rows = max(min(Lk - t * kKBlk, kKBlk), 0);
+    const int nbytes = __builtin_amdgcn_readfirstlane(rows * (int)(sl * 2) - (rows > 0 ? (int)(sl * 2) - 2 * kD : 0));
+    // wave-uniform by construction; readfirstlane lets the compiler see it (no waterfall loops, T20)
+    const uintptr_t addr = (uintptr_t)(base + (int64_t)min(t, ntiles - 1) * kKBlk * sl);
+    const uintptr_t ua = ((uintptr_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(addr >> 32)) << 32) |
+                         (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)addr);
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)ua, (short)0, nbytes, 0x00020000);
+    const int off = kv ? stv_off : stk_off, step = kv ? stv_step : stk_step;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      st[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + i * step, 0, 0));
+  };
+  // LDS slot bases (bytes): K slot j at j * kKBuf, V slot j at 3 kKBuf + j * kVBuf
+  const int k_wr = srow * kKStride + sch * 16;
+  const int v_wr = 3 * kKBuf + srow * kVStride + sch * 16;
+  auto write_k = [&](int slot) __attribute__((always_inline)) {
+    char* dst = smem + k_wr + slot * kKBuf;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(dst + 16 * i * kKStride) = st[i];
+  };
+  auto write_v = [&](int slot) __attribute__((always_inline)) {
+    char* dst = smem + v_wr + slot * kVBuf;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(dst + 16 * i * kVStride) = st[i];
+  };
+
+  // per-lane LDS read offsets (the slot base is added once per iteration, the rest is immediate)
+  const int k_rd = l31 * kKStride + 16 * hl;
+  const int grp = lane >> 4, gi = lane & 15;
+  const int tq = gi >> 2, tp = gi & 3;
+  const int v_rd = 3 * kKBuf + (4 * (grp >> 1) + tq) * kVStride + 32 * (grp & 1) + 8 * tp;
+
+  auto k_frag = [&](const char* kb, int kt, int s) __attribute__((always_inline)) {
+    return *reinterpret_cast<const bf16x8*>(kb + kt * 32 * kKStride + 32 * s);
+  };
+  // V^T fragment of k-step ks (16 keys) and d-block db: two transposed 4x16-bit reads
+  auto v_frag = [&](const char* vb, int ks, int db) __attribute__((always_inline)) {
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const int off = 16 * ks * kVStride + 64 * db;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds_char_ptr)(vb + off));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds_char_ptr)(vb + off + 8 * kVStride));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, r);
+  };
+
+  f32x16 S[2][2];     // [half parity][q-block]: S^T of a 32-key half tile
+  bf16x8 P[2][2][2];  // [half parity][q-block][k-step]: P^T of a half tile as P.V B operands
+  const bf16x8 zero8 = {};
+
+  // ---- prologue: K(0), K(1), V(0) -> slots 0, 1, 0; V slot 2 zeroed (V(-1) of the P.V(-1) of
+  // sub-step 0, with P = 0); S(0) = QK^T(half 0) ----
+  load_tile(0, 0);
+  write_k(0);
+  load_tile(0, 1);
+  write_k(1);
+  load_tile(1, 0);
+  write_v(0);
+  {
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    st[0] = z; st[1] = z; st[2] = z; st[3] = z;
+    write_v(2);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const bf16x8 kf = k_frag(smem + k_rd, 0, s);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (s == 0) mfma_s_init(S[0][j], kf, qf[j][s]);
+      else mfma_s_acc(S[0][j], kf, qf[j][s]);
+    }
+  }
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");  // S(0) -> the first softmax reads
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int sp = 0; sp < 2; ++sp) P[1][j][sp] = zero8;
+
+  // one sub-step: half i = 2t + SUB. QK^T(i+1) from K rows kq (32-row half kt_q) -> S[SUB^1];
+  // softmax S[SUB] -> P[SUB]; P.V(i-1) from V half vh of the rows at vb with P[SUB^1]
+  auto sub_step = [&](auto SUBC, auto MASKC, int i, const char* kq, int kt_q, const char* vb,
+                      int vh) __attribute__((always_inline)) {
+    constexpr int c = decltype(SUBC)::value;  // parity of half i
+    constexpr int n = c ^ 1;
+    if (decltype(MASKC)::value && 32 * (i + 1) > Lk) {  // last tile only: keys >= Lk get -inf scores
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hl;
+          if (key >= Lk) S[c][j][r] = -INFINITY;
+        }
+    }
+    float psum[2] = {0.f, 0.f};
+    // LDS operands: all eight K fragments of the sub-step up front, V fragments two groups ahead
+    bf16x8 kfr[8], vfr[8];
+#pragma unroll
+    for (int g = 0; g < 8; ++g) kfr[g] = k_frag(kq, kt_q, g);
+    vfr[0] = v_frag(vb, 2 * vh, 0);
+    vfr[1] = v_frag(vb, 2 * vh, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    // the issue stream, fixed by sched_barrier(0) fences: per group g, four (MFMA, VALU slice) pairs;
+    // slice m handles score e = m of the group's four (fma, exp, row-sum add; a bf16 pack per pair)
+    static_for<8>([&](auto GC) __attribute__((always_inline)) {
+      constexpr int g = decltype(GC)::value;
+      constexpr int pk = g >> 1, jj = pk & 1, sp = pk >> 1, hf = g & 1;
+      float pv[4];
+      static_for<4>([&](auto MC) __attribute__((always_inline)) {
+        constexpr int m = decltype(MC)::value;
+        if constexpr (m < 2) {  // QK^T(i+1), d-step g, q-block m
+          if constexpr (g == 0) mfma_s_init(S[n][m], kfr[g], qf[m][g]);
+          else mfma_s_acc(S[n][m], kfr[g], qf[m][g]);
+        } else {  // P.V(i-1): k-step g >> 2 of the half, d-block g & 3, q-block m - 2
+          o[g & 3][m - 2] =
+              __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr[g], P[n][m - 2][g >> 2], o[g & 3][m - 2], 0, 0, 0);
+        }
+        if constexpr (m == 0 && g + 2 < 8) vfr[g + 2] = v_frag(vb, 2 * vh + ((g + 2) >> 2), (g + 2) & 3);
+        // softmax of half i: score e = m of pack (q-block jj, k-step sp), half hf
+        const float sv = S[c][jj][8 * sp + 4 * hf + m];
+        pv[m] = __builtin_amdgcn_exp2f(kPre ? sv : fmaf(sv, a.scale_log2, -m_sh[jj]));
+        psum[jj] += pv[m];
+        if constexpr (m & 1) {
+          P[c][jj][sp][4 * hf + m - 1] = static_cast<__bf16>(pv[m - 1]);
+          P[c][jj][sp][4 * hf + m] = static_cast<__bf16>(pv[m]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    });
+    l_run[0] += psum[0];
+    l_run[1] += psum[1];
+  };
+
+  // iteration t: two sub-steps, stage K(t+2) and V(t+1), one barrier; only the last tile can be
+  // ragged, so the main loop carries no masking (one basic block for the scheduler)
+  auto iteration = [&](auto MASKC, int t, int slot) __attribute__((always_inline)) {
+    const int s1 = slot == 2 ? 0 : slot + 1, s2 = slot == 0 ? 2 : slot - 1;  // (t+1) % 3, (t+2) % 3
+    const char* k_cur = smem + k_rd + slot * kKBuf;
+    const char* k_nxt = smem + k_rd + s1 * kKBuf;
+    const char* v_prv = smem + v_rd + s2 * kVBuf;
+    const char* v_cur = smem + v_rd + slot * kVBuf;
+    load_tile(0, t + 2);
+    // sub-step 0: QK^T(2t+1) = K(t) rows 32..63, softmax(2t), P.V(2t-1) = V(t-1) rows 32..63
+    sub_step(std::integral_constant<int, 0>{}, MASKC, 2 * t, k_cur, 1, v_prv, 1);
+    write_k(s2);
+    load_tile(1, t + 1);
+    // sub-step 1: QK^T(2t+2) = K(t+1) rows 0..31, softmax(2t+1), P.V(2t) = V(t) rows 0..31
+    sub_step(std::integral_constant<int, 1>{}, MASKC, 2 * t + 1, k_nxt, 0, v_cur, 0);
+    write_v(s1);
+    __syncthreads();
+    return s1;
+  };
+  int slot = 0;  // t % 3
+  for (int t = 0; t < ntiles - 1; ++t) slot = iteration(std::false_type{}, t, slot);
+  iteration(std::true_type{}, ntiles - 1, slot);
+
+  // ---- drain: P.V(2 ntiles - 1) = V(ntiles - 1) rows 32..63 with P[1] ----
+  {
+    const int sl = (ntiles - 1) % 3;
+    const char* vb = smem + v_rd + sl * kVBuf;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      const bf16x8 vf = v_frag(vb, 2 + (g >> 2), g & 3);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        o[g & 3][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, P[1][j][g >> 2], o[g & 3][j], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue: O = O^T / l, row q, d = 32 db + 8 g + 4 hl + (0..3) ----
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const float l_tot = wave_swap_sum(l_run[j]);
+    // contract guard: norm bounds below the real norms can only show as an overflowed row sum
+    // (moderate violations are exact by shift invariance): poison the row (NaN); never taken
+    // under the contract
+    const float inv = l_tot < 3.0e38f ? 1.f / l_tot : __uint_as_float(0x7fc00000u);
+    if (q_row[j] >= a.Lq) continue;
+    if (a.nsplit > 1) {
+      const int64_t row = ((int64_t)(split * a.B + b) * a.H + h) * a.Lq + q_row[j];
+      float* op = a.o_part + row * kD;
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          f32x4 w;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[e] = o[db][j][4 * g + e] * inv;
+          *reinterpret_cast<f32x4*>(op + 32 * db + 8 * g + 4 * hl) = w;
+        }
+      if (hl == 0) a.lse_part[row] = m_sh[j] + __log2f(l_tot);
+    } else {
+      unsigned short* op = a.o + b * a.o_sb + h * a.o_sh + (int64_t)q_row[j] * a.o_sl;
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          u16x4 w;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[e] = f2bf(o[db][j][4 * g + e] * inv);
+          *reinterpret_cast<u16x4*>(op + 32 * db + 8 * g + 4 * hl) = w;
+        }
+    }
+  }
+}
+
 // O[b, q, h, :] = sum_s w_s O_s / sum_s w_s with w_s = exp2(lse_s - max_s lse_s): the key-range
 // partials of one (b, h, q) row combined exactly as the online softmax would have. One thread per
 // 4 head-dim elements (32 threads per row); HBM-bound.
@@ -494,6 +802,17 @@ __global__ void __launch_bounds__(256) attn_merge_splits(const float* __restrict
 }
 
 int g_num_cus = 0;
+
+// which bounded/prescaled kernel runs: CP25_ATTN_KERNEL=2w (attn_fwd_d128, two waves per SIMD) or
+// 1w (attn_fwd_1w); read once
+int g_use_1w = -1;
+bool use_1w() {
+  if (g_use_1w < 0) {
+    const char* e = getenv("CP25_ATTN_KERNEL");
+    g_use_1w = (e && e[0] == '2') ? 0 : 1;
+  }
+  return g_use_1w == 1;
+}
 
 int num_cus() {
   if (g_num_cus == 0) {
@@ -591,10 +910,16 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
 #endif
   const int64_t nwg = (int64_t)a.nqb * B * H * n_split;
   if (nwg > 0x7fffffff) return CP25_ERR_INVAL;
-  auto kernel = prescaled ? (Lk <= 4096 ? attn_fwd_d128<1, true, true> : attn_fwd_d128<0, true, true>)
-                : Lk <= 4096 ? (fixed ? attn_fwd_d128<1, true> : attn_fwd_d128<1, false>)
-                             : (fixed ? attn_fwd_d128<0, true> : attn_fwd_d128<0, false>);
-  hipLaunchKernelGGL(kernel, dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
+  if ((prescaled || fixed) && use_1w()) {
+    auto kernel = prescaled ? (Lk <= 4096 ? attn_fwd_1w<1, true> : attn_fwd_1w<0, true>)
+                            : (Lk <= 4096 ? attn_fwd_1w<1, false> : attn_fwd_1w<0, false>);
+    hipLaunchKernelGGL(kernel, dim3((unsigned)nwg), dim3(kThreads1w), 0, stream, a);
+  } else {
+    auto kernel = prescaled ? (Lk <= 4096 ? attn_fwd_d128<1, true, true> : attn_fwd_d128<0, true, true>)
+                  : Lk <= 4096 ? (fixed ? attn_fwd_d128<1, true> : attn_fwd_d128<1, false>)
+                               : (fixed ? attn_fwd_d128<0, true> : attn_fwd_d128<0, false>);
+    hipLaunchKernelGGL(kernel, dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
+  }
   CP25_LAUNCH_CHECK();
   if (n_split > 1) {
     const int64_t threads = rows * 32;
