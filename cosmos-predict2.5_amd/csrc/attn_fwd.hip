@@ -482,13 +482,16 @@ constexpr int kThreads1w = 256;
 
 // S^T MFMAs of attn_fwd_1w as inline asm: the scores must land in arch VGPRs (the softmax reads them
 // with VALU; the builtin puts them in the accumulator file and copies them back, 32 v_accvgpr_read per
-// half tile), with the Q operand held in the accumulator file. Hazard (MFMA D -> VALU read): every
-// consumer of these results is issued >= 4 MFMAs later (next sub-step) or behind explicit s_nops.
+// half tile), with the Q operand held in the accumulator file. hipcc pads nothing inside an asm
+// string, so the string carries its own wait states: `s_nop 1` ahead of the MFMA covers a
+// v_accvgpr_write of the Q operand (or a VALU write of K) just before it (VALU -> MFMA operand: 2
+// states). MFMA D -> VALU read: every consumer of these results is issued >= 3 MFMAs later (the next
+// sub-step's softmax) or behind the explicit s_nops after the prologue.
 __device__ __forceinline__ void mfma_s_init(f32x16& d, const bf16x8& k, const bf16x8& q) {
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(k), "a"(q));
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(k), "a"(q));
 }
 __device__ __forceinline__ void mfma_s_acc(f32x16& d, const bf16x8& k, const bf16x8& q) {
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(k), "a"(q));
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(k), "a"(q));
 }
 constexpr int kLds1w = 3 * kKBuf + 3 * kVBuf;  // 113664
 
@@ -803,13 +806,15 @@ __global__ void __launch_bounds__(256) attn_merge_splits(const float* __restrict
 
 int g_num_cus = 0;
 
-// which bounded/prescaled kernel runs: CP25_ATTN_KERNEL=2w (attn_fwd_d128, two waves per SIMD) or
-// 1w (attn_fwd_1w); read once
+// which bounded/prescaled kernel runs: attn_fwd_d128 (two waves per SIMD, ping-pong; the default) or,
+// with CP25_ATTN_KERNEL=1w, attn_fwd_1w (one wave per SIMD). Measured at the metric shape (same box,
+// DESIGN.md §3): 1w 172 ms vs 2w 159.5 ms per launch; 1w holds 2.06 GHz but its MFMA pipe is busy
+// only 52 % of cycles (2w: 69.5 % at 1.68 GHz). Read once.
 int g_use_1w = -1;
 bool use_1w() {
   if (g_use_1w < 0) {
     const char* e = getenv("CP25_ATTN_KERNEL");
-    g_use_1w = (e && e[0] == '2') ? 0 : 1;
+    g_use_1w = (e && e[0] == '1') ? 1 : 0;
   }
   return g_use_1w == 1;
 }

@@ -11,7 +11,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNEL = "attn_fwd_d128<0"  # self-attention instantiations (<0, true>: bounded shift)
+KERNELS = ("attn_fwd_d128<0", "attn_fwd_1w<0")  # self-attention instantiations (d128 <0, true>: bounded shift)
 FLOP = 4.0 * 2 * 16 * 109120 * 109120 * 128
 ALGO_BYTES = 4 * 2 * 16 * 109120 * 128 * 2  # Q, K, V read once, O written once (bf16)
 
@@ -22,7 +22,7 @@ def load(out):
         per = defaultdict(lambda: defaultdict(float))
         span = {}
         for r in csv.DictReader(open(f)):
-            if KERNEL not in r["Kernel_Name"]:
+            if not any(k in r["Kernel_Name"] for k in KERNELS):
                 continue
             d = int(r["Dispatch_Id"])
             per[d][r["Counter_Name"]] += float(r["Counter_Value"])
