@@ -48,8 +48,11 @@ def _report(name, hip, ref, truth):
     return d
 
 
-def test_full_depth_2b_forward(device, net2b):
-    """One 28-block forward at config-1 geometry (cond frame t 0.1, the others mid-trajectory)."""
+@pytest.mark.parametrize("exact_q", [False, True])
+def test_full_depth_2b_forward(device, net2b, exact_q):
+    """One 28-block forward at config-1 geometry (cond frame t 0.1, the others mid-trajectory); both
+    self-attention query roundings (exact_q: q rounded where the reference rounds it; default: q * c
+    rounded once, the prescaled kernel)."""
     cfg, sd = net2b
     g = torch.Generator().manual_seed(31)
     T, H, W = 3, 32, 32
@@ -64,9 +67,10 @@ def test_full_depth_2b_forward(device, net2b):
         truth = odit.dit_forward(c, sd, x, t, ctx, mask)
     net = MinimalV1LVGDiT(cfg, device=device)
     net.load_state_dict(sd)
+    net.exact_q_rounding = exact_q
     hip = net(x.to(device).to(torch.bfloat16), t.to(device), ctx.to(device),
               condition_video_input_mask_B_C_T_H_W=mask.to(device)).cpu()
-    d = _report("28-block 2B forward (config-1 geometry)", hip, ref, truth)
+    d = _report(f"28-block 2B forward (config-1 geometry, exact_q={exact_q})", hip, ref, truth)
     assert torch.isfinite(hip).all()
     # measured (MI355X, round 2): hip-truth 1.162e-2, ref-truth 1.164e-2, hip-ref 8.81e-3
     assert d["hip_truth"] <= 1.1 * d["ref_truth"], d
