@@ -35,7 +35,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "frames/sec, Predict2.5-2B Image2World 720p×121f, 35 UniPC steps, CP=1/8"
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 MFMA
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1", "attn_pmc_r1e", "SUMMARY.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r2", "attn_pmc", "SUMMARY.json")
 
 
 def parse():

@@ -31,6 +31,8 @@ def main():
                     help="RMS-normalised q/k rows (as the DiT's q/k norm leaves them) and their norm bounds: the "
                          "bounded-shift softmax (cp25_attn_fwd_bounded)")
     ap.add_argument("--normed", action="store_true", help="RMS-normalised q/k rows without passing the bounds")
+    ap.add_argument("--prescaled", action="store_true",
+                    help="with --bounded: q carries scale*log2(e) (the DiT's default form, cp25_attn_fwd_prescaled)")
     ap.add_argument("--lib", default="", help="lab build of libcp25.so to load instead of the in-tree one")
     a = ap.parse_args()
     if a.lib:
@@ -55,6 +57,12 @@ def main():
         for t in (q, k):  # RMSNorm with unit weight, in place, per head row
             t.copy_((t.float() * torch.rsqrt(t.float().pow(2).mean(-1, keepdim=True) + 1e-6)).to(torch.bfloat16))
         nb = (128 ** 0.5 * 1.02, 128 ** 0.5 * 1.02) if a.bounded else None
+    pre = {}
+    if a.prescaled:
+        c = 128 ** -0.5 * 1.4426950408889634
+        q.copy_((q.float() * c).to(torch.bfloat16))
+        nb = (nb[0] * c, nb[1])
+        pre = dict(prescaled=True)
     # correctness of the loaded build on a small shape (ragged length) vs fp32 math
     gc = torch.Generator(device=dev).manual_seed(1)
     qc, kc, vc = (torch.randn(1, 1000, 2, 128, device=dev, generator=gc).to(torch.bfloat16) for _ in range(3))
@@ -64,20 +72,20 @@ def main():
     oc = N.attn_fwd(qc, kc, vc, n_split=1, norm_bounds=ncb).float()
     check = float((oc - ref).norm() / ref.norm())
     ns = a.split or N.attn_plan(a.B, a.H, a.L, Lk)
-    o = N.attn_fwd(q, k, v, n_split=ns, norm_bounds=nb)
+    o = N.attn_fwd(q, k, v, n_split=ns, norm_bounds=nb, **pre)
     torch.cuda.synchronize()
     st = torch.cuda.current_stream()
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     e0.record(st)
     for _ in range(a.iters):
-        N.attn_fwd(q, k, v, out=o, n_split=ns, norm_bounds=nb)
+        N.attn_fwd(q, k, v, out=o, n_split=ns, norm_bounds=nb, **pre)
     e1.record(st)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
     flop = 4.0 * a.B * a.H * a.L * Lk * 128
     print(json.dumps({"kernel": "attn_fwd", "B": a.B, "H": a.H, "Lq": a.L, "Lk": Lk, "fused": a.fused,
-                      "zeros": a.zeros, "bounded": a.bounded, "normed": a.normed or a.bounded, "split": ns, "iters": a.iters, "lib": os.path.basename(a.lib) or "libcp25.so", "ms": ms,
+                      "zeros": a.zeros, "bounded": a.bounded, "prescaled": a.prescaled, "normed": a.normed or a.bounded, "split": ns, "iters": a.iters, "lib": os.path.basename(a.lib) or "libcp25.so", "ms": ms,
                       "tflops": flop / ms / 1e9, "check_rel_l2": check}))
 
 

@@ -16,5 +16,5 @@ i=0
 for c in "${passes[@]}"; do
   i=$((i + 1))
   timeout -k 10 150 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$out" -o p$i -- \
-    python tools/bench_attn.py --L 109120 --B 2 --iters 1 --bounded > "$out/p$i.log" 2>&1
+    python3 tools/bench_attn.py --L 109120 --B 2 --iters 1 --bounded --fused --prescaled > "$out/p$i.log" 2>&1
 done

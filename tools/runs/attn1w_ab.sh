@@ -10,3 +10,5 @@ done
 CP25_ATTN_KERNEL=1w timeout -k 10 120 python tools/bench_attn.py --L 109120 --Lk 512 --bounded --iters 20 >> gpurun_out/attn1w_ab.log 2>&1
 CP25_ATTN_KERNEL=2w timeout -k 10 120 python tools/bench_attn.py --L 109120 --Lk 512 --bounded --iters 20 >> gpurun_out/attn1w_ab.log 2>&1
 cat gpurun_out/attn1w_ab.log | cut -c1-400
+timeout -k 10 400 python -u -m pytest tests/test_configs_gpu.py -x -v -s --timeout 300 --timeout-method thread > gpurun_out/configs_gpu.log 2>&1
+rc=$?; grep -E "rel-L2|passed|failed|Error" gpurun_out/configs_gpu.log | tail -8; exit $rc
