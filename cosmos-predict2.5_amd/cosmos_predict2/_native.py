@@ -64,6 +64,7 @@ SIGNATURES = {
     "cp25_head_rmsnorm_rope_scaled": [_P, _I64, _I64, _I, _I, _I, _P, _P, _P, _P, _I64, _F, _F, _P],
     "cp25_copy_rows": [_P, _I64, _P, _I64, _I64, _I64, _P],
     "cp25_gelu": [_P, _I64, _P],
+    "cp25_gemm_epi": [_P, _I64, _P, _I64, _P, _I64, _I, _I, _I, _I, _P],
     "cp25_quant_fp8_rows": [_P, _P, _P, _I64, _I64, _P],
     "cp25_gelu_quant_fp8": [_P, _P, _P, _I64, _I64, _P],
     "cp25_patchify": [_P, _P, _P, _P, _P, _I64, _I64, _I64, _P],
@@ -286,6 +287,34 @@ def gelu_(x: torch.Tensor) -> torch.Tensor:
         raise ValueError("gelu_ expects a contiguous bf16 tensor")
     _check("cp25_gelu", lib.cp25_gelu(_ptr(x), x.numel(), _stream(x.device)))
     return x
+
+
+EPI_NONE, EPI_GELU = 0, 1
+
+
+def gemm_supported(N: int, K: int) -> bool:
+    """Shapes cp25_gemm_epi is built for (N multiple of 256, K of 64); others stay on the library GEMM."""
+    return N % 256 == 0 and K % 64 == 0
+
+
+def gemm_epi(a: torch.Tensor, w: torch.Tensor, epilogue: int = EPI_NONE, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[M, N] = epi(a[M, K] w[N, K]^T) in bf16 (cp25_gemm_epi); EPI_GELU applies the exact-erf GELU to the
+    bf16 product (GPT2FeedForward layer1 + activation)."""
+    lib = load_library()
+    if a.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        raise ValueError("gemm_epi expects bf16 operands")
+    if a.dim() != 2 or w.dim() != 2 or a.shape[1] != w.shape[1] or a.stride(1) != 1 or w.stride(1) != 1:
+        raise ValueError(f"gemm_epi shapes a{tuple(a.shape)} w{tuple(w.shape)}: need [M, K] x [N, K], K contiguous")
+    M, K = a.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    if tuple(out.shape) != (M, N) or out.stride(1) != 1:
+        raise ValueError(f"gemm_epi out {tuple(out.shape)} != ({M}, {N})")
+    rc = lib.cp25_gemm_epi(_ptr(a), a.stride(0), _ptr(w), w.stride(0), _ptr(out), out.stride(0), M, N, K, int(epilogue),
+                           _stream(a.device))
+    _check("cp25_gemm_epi", rc)
+    return out
 
 
 def quant_fp8_rows(x: torch.Tensor, gelu: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:

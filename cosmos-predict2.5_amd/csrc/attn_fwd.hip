@@ -475,9 +475,11 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
 // reads of row-major V) and the same padded LDS rows; bounded-shift / prescaled softmax only (the
 // DiT's forms; the online-max form stays on attn_fwd_d128).
 // One loop iteration t = two sub-steps (halves 2t, 2t+1) and one barrier; it reads K(t), K(t+1),
-// V(t-1), V(t) and stages K(t+2), V(t+1) (register-staged by all four waves: loads at the top of a
-// sub-step, LDS writes at its end) into a 3-deep ring, K(j) / V(j) in slot j % 3: K(t+2) overwrites
-// K(t-1), V(t+1) overwrites V(t-2), both last read in iteration t-1.
+// V(t-1), V(t) and writes K(t+2), V(t+1) into a 3-deep LDS ring (K(j) / V(j) in slot j % 3: K(t+2)
+// overwrites K(t-1), V(t+1) overwrites V(t-2), both last read in iteration t-1). Register-staged by all
+// four waves one iteration ahead: the iteration opens with the LDS writes of the tiles loaded in the
+// previous iteration, then issues the loads of K(t+3) / V(t+2), which stay in flight across the
+// barrier (the global latency is covered by a whole iteration).
 constexpr int kThreads1w = 256;
 
 // S^T MFMAs of attn_fwd_1w as inline asm: the scores must land in arch VGPRs (the softmax reads them
@@ -559,9 +561,19 @@ __global__ void __launch_bounds__(kThreads1w, 1) attn_fwd_1w(AttnArgs a) {
   const int srow = tid >> 4, sch = tid & 15;
   const int stk_off = (int)(srow * a.k_sl * 2) + sch * 16, stk_step = (int)(16 * a.k_sl * 2);
   const int stv_off = (int)(srow * a.v_sl * 2) + sch * 16, stv_step = (int)(16 * a.v_sl * 2);
-  u32x4 st[4];
+  u32x4 stk[4], stv[4];  // staged K(t+3) / V(t+2), in flight across the iteration's barrier
   // tile t of K (kv = 0) or V (kv = 1); tiles past the end read as zeros (empty descriptor)
-  auto load_tile = [&](int kv, int t) __attribute__((always_inline)) {
+  auto tile_rsrc = [&](int kv, int t) __attribute__((always_inline)) {
+    const int64_t sl = kv ? a.v_sl : a.k_sl;
+    const unsigned short* base = kv ? vp : kp;
+    const int rows = max(min(Lk - t * kKBlk, kKBlk), 0);
+    const int nbytes = __builtin_amdgcn_readfirstlane(rows * (int)(sl * 2) - (rows > 0 ? (int)(sl * 2) - 2 * kD : 0));
+    const uintptr_t addr = (uintptr_t)(base + (int64_t)min(t, ntiles - 1) * kKBlk * sl);
+    const uintptr_t ua = ((uintptr_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(addr >> 32)) << 32) |
+                         (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)addr);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)ua, (short)0, nbytes, 0x00020000);
+  };
+  auto load_tile = [&](int kv, int t, u32x4* st) __attribute__((always_inline)) {
     const int64_t sl = kv ? a.v_sl : a.k_sl;
     const unsigned short* base = kv ? vp : kp;
     // rows of tile t inside [0, Lk) (0 past the end), branch-free: the descriptor's range check
@@ -581,12 +593,12 @@ __global__ void __launch_bounds__(kThreads1w, 1) attn_fwd_1w(AttnArgs a) {
   // LDS slot bases (bytes): K slot j at j * kKBuf, V slot j at 3 kKBuf + j * kVBuf
   const int k_wr = srow * kKStride + sch * 16;
   const int v_wr = 3 * kKBuf + srow * kVStride + sch * 16;
-  auto write_k = [&](int slot) __attribute__((always_inline)) {
+  auto write_k = [&](int slot, const u32x4* st) __attribute__((always_inline)) {
     char* dst = smem + k_wr + slot * kKBuf;
 #pragma unroll
     for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(dst + 16 * i * kKStride) = st[i];
   };
-  auto write_v = [&](int slot) __attribute__((always_inline)) {
+  auto write_v = [&](int slot, const u32x4* st) __attribute__((always_inline)) {
     char* dst = smem + v_wr + slot * kVBuf;
 #pragma unroll
     for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(dst + 16 * i * kVStride) = st[i];
@@ -618,17 +630,19 @@ __global__ void __launch_bounds__(kThreads1w, 1) attn_fwd_1w(AttnArgs a) {
 
   // ---- prologue: K(0), K(1), V(0) -> slots 0, 1, 0; V slot 2 zeroed (V(-1) of the P.V(-1) of
   // sub-step 0, with P = 0); S(0) = QK^T(half 0) ----
-  load_tile(0, 0);
-  write_k(0);
-  load_tile(0, 1);
-  write_k(1);
-  load_tile(1, 0);
-  write_v(0);
+  load_tile(0, 0, stk);
+  write_k(0, stk);
+  load_tile(0, 1, stk);
+  write_k(1, stk);
+  load_tile(1, 0, stv);
+  write_v(0, stv);
   {
     const u32x4 z = {0u, 0u, 0u, 0u};
-    st[0] = z; st[1] = z; st[2] = z; st[3] = z;
-    write_v(2);
+    const u32x4 zs[4] = {z, z, z, z};
+    write_v(2, zs);
   }
+  load_tile(0, 2, stk);  // written at the top of iteration 0
+  load_tile(1, 1, stv);
   __syncthreads();
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
@@ -647,8 +661,13 @@ __global__ void __launch_bounds__(kThreads1w, 1) attn_fwd_1w(AttnArgs a) {
 
   // one sub-step: half i = 2t + SUB. QK^T(i+1) from K rows kq (32-row half kt_q) -> S[SUB^1];
   // softmax S[SUB] -> P[SUB]; P.V(i-1) from V half vh of the rows at vb with P[SUB^1]
-  auto sub_step = [&](auto SUBC, auto MASKC, int i, const char* kq, int kt_q, const char* vb,
-                      int vh) __attribute__((always_inline)) {
+  // LDS operands carried from one sub-step into the next: the first four K fragments and the first
+  // two V fragments of a sub-step are read during the previous one (its groups 4..7), so no sub-step
+  // opens on an LDS latency; every tile they read was written before the previous barrier
+  bf16x8 ck[4], cv[2];
+  auto sub_step = [&](auto SUBC, auto MASKC, int i, const char* kq, int kt_q, const char* vb, int vh,
+                      const char* kq_n, int kt_n, const char* vb_n, int vh_n,
+                      auto&& stage) __attribute__((always_inline)) {
     constexpr int c = decltype(SUBC)::value;  // parity of half i
     constexpr int n = c ^ 1;
     if (decltype(MASKC)::value && 32 * (i + 1) > Lk) {  // last tile only: keys >= Lk get -inf scores
@@ -661,12 +680,12 @@ __global__ void __launch_bounds__(kThreads1w, 1) attn_fwd_1w(AttnArgs a) {
         }
     }
     float psum[2] = {0.f, 0.f};
-    // LDS operands: all eight K fragments of the sub-step up front, V fragments two groups ahead
+    // LDS operands: K fragments four groups ahead, V fragments two groups ahead, the first ones carried
     bf16x8 kfr[8], vfr[8];
 #pragma unroll
-    for (int g = 0; g < 8; ++g) kfr[g] = k_frag(kq, kt_q, g);
-    vfr[0] = v_frag(vb, 2 * vh, 0);
-    vfr[1] = v_frag(vb, 2 * vh, 1);
+    for (int g = 0; g < 4; ++g) kfr[g] = ck[g];
+    vfr[0] = cv[0];
+    vfr[1] = cv[1];
     __builtin_amdgcn_sched_barrier(0);
     // the issue stream, fixed by sched_barrier(0) fences: per group g, four (MFMA, VALU slice) pairs;
     // slice m handles score e = m of the group's four (fma, exp, row-sum add; a bf16 pack per pair)
@@ -684,6 +703,10 @@ __global__ void __launch_bounds__(kThreads1w, 1) attn_fwd_1w(AttnArgs a) {
               __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr[g], P[n][m - 2][g >> 2], o[g & 3][m - 2], 0, 0, 0);
         }
         if constexpr (m == 0 && g + 2 < 8) vfr[g + 2] = v_frag(vb, 2 * vh + ((g + 2) >> 2), (g + 2) & 3);
+        if constexpr (m == 1 && g < 4) kfr[g + 4] = k_frag(kq, kt_q, g + 4);
+        if constexpr (m == 1 && g >= 4) ck[g - 4] = k_frag(kq_n, kt_n, g - 4);  // next sub-step's
+        if constexpr (m == 3 && g >= 6) cv[g - 6] = v_frag(vb_n, 2 * vh_n, g - 6);
+        if constexpr (m == 2 && g < 4) stage(g);  // one staged 16-B piece per group, in the MFMA shadow
         // softmax of half i: score e = m of pack (q-block jj, k-step sp), half hf
         const float sv = S[c][jj][8 * sp + 4 * hf + m];
         pv[m] = __builtin_amdgcn_exp2f(kPre ? sv : fmaf(sv, a.scale_log2, -m_sh[jj]));
@@ -707,17 +730,33 @@ __global__ void __launch_bounds__(kThreads1w, 1) attn_fwd_1w(AttnArgs a) {
     const char* k_nxt = smem + k_rd + s1 * kKBuf;
     const char* v_prv = smem + v_rd + s2 * kVBuf;
     const char* v_cur = smem + v_rd + slot * kVBuf;
-    load_tile(0, t + 2);
+    // staging, one 16-B piece per MFMA group, spread over the groups in the MFMA shadow (clustered at
+    // the iteration start, the 8 loads + 8 LDS writes left the matrix pipe idle for ~500 cycles): piece
+    // i of K(t+2) / V(t+1), loaded one iteration ago, goes to LDS, then piece i of K(t+3) / V(t+2) is
+    // loaded into the same registers and flies across this iteration and its barrier
+    const auto rk = tile_rsrc(0, t + 3);
+    const auto rv = tile_rsrc(1, t + 2);
+    char* const kdst = smem + k_wr + s2 * kKBuf;
+    char* const vdst = smem + v_wr + s1 * kVBuf;
     // sub-step 0: QK^T(2t+1) = K(t) rows 32..63, softmax(2t), P.V(2t-1) = V(t-1) rows 32..63
-    sub_step(std::integral_constant<int, 0>{}, MASKC, 2 * t, k_cur, 1, v_prv, 1);
-    write_k(s2);
-    load_tile(1, t + 1);
+    sub_step(std::integral_constant<int, 0>{}, MASKC, 2 * t, k_cur, 1, v_prv, 1, k_nxt, 0, v_cur, 0, [&](int p) {
+      *reinterpret_cast<u32x4*>(kdst + 16 * p * kKStride) = stk[p];
+      stk[p] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, stk_off + p * stk_step, 0, 0));
+    });
     // sub-step 1: QK^T(2t+2) = K(t+1) rows 0..31, softmax(2t+1), P.V(2t) = V(t) rows 0..31
-    sub_step(std::integral_constant<int, 1>{}, MASKC, 2 * t + 1, k_nxt, 0, v_cur, 0);
-    write_v(s1);
+    // (next: sub-step 0 of iteration t+1 = K(t+1) rows 32..63, V(t) rows 32..63)
+    sub_step(std::integral_constant<int, 1>{}, MASKC, 2 * t + 1, k_nxt, 0, v_cur, 0, k_nxt, 1, v_cur, 1, [&](int p) {
+      *reinterpret_cast<u32x4*>(vdst + 16 * p * kVStride) = stv[p];
+      stv[p] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, stv_off + p * stv_step, 0, 0));
+    });
     __syncthreads();
     return s1;
   };
+  // carried operands of iteration 0's sub-step 0: K(0) rows 32..63, V(-1) (zeroed slot 2) rows 32..63
+#pragma unroll
+  for (int g = 0; g < 4; ++g) ck[g] = k_frag(smem + k_rd, 1, g);
+  cv[0] = v_frag(smem + v_rd + 2 * kVBuf, 2, 0);
+  cv[1] = v_frag(smem + v_rd + 2 * kVBuf, 2, 1);
   int slot = 0;  // t % 3
   for (int t = 0; t < ntiles - 1; ++t) slot = iteration(std::false_type{}, t, slot);
   iteration(std::true_type{}, ntiles - 1, slot);
@@ -807,9 +846,11 @@ __global__ void __launch_bounds__(256) attn_merge_splits(const float* __restrict
 int g_num_cus = 0;
 
 // which bounded/prescaled kernel runs: attn_fwd_d128 (two waves per SIMD, ping-pong; the default) or,
-// with CP25_ATTN_KERNEL=1w, attn_fwd_1w (one wave per SIMD). Measured at the metric shape (same box,
-// DESIGN.md §3): 1w 172 ms vs 2w 159.5 ms per launch; 1w holds 2.06 GHz but its MFMA pipe is busy
-// only 52 % of cycles (2w: 69.5 % at 1.68 GHz). Read once.
+// with CP25_ATTN_KERNEL=1w, attn_fwd_1w (one wave per SIMD). Measured at the metric shape, prescaled
+// form, same box: 1w 151.0 ms vs 2w 146.3 ms per launch (first version 172 vs 159.5;
+// then the staging spread over the MFMA groups and carried LDS operands); 1w holds ~1.94 GHz with the
+// MFMA pipe busy 62 % of cycles, 2w ~1.62 GHz at 78 %. Without any K/V staging the 1w loop runs
+// 121-134 ms: what is left is hiding the global loads without a second wave. Read once.
 int g_use_1w = -1;
 bool use_1w() {
   if (g_use_1w < 0) {

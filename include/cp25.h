@@ -135,6 +135,20 @@ int cp25_copy_rows(const void* src, int64_t src_stride, void* dst, int64_t dst_s
  * Replaces: GPT2FeedForward activation, minimal_v4_dit.py:249-254. */
 int cp25_gelu(void* x, int64_t n, hipStream_t stream);
 
+/* ---------------------------------------------------------------- block projections (GEMM + epilogue)
+ * C[M, N] = epi(A[M, K] W[N, K]^T): A, W, C bf16 row-major with leading dims lda / ldw / ldc (elements,
+ * multiples of 8, pointers 16-B aligned), fp32 accumulation, one bf16 rounding of the product.
+ * epilogue CP25_EPI_NONE: C = bf16(A W^T); CP25_EPI_GELU: C = bf16(gelu_erf(bf16(A W^T))), the same
+ * arithmetic as cp25_gelu on the stored product. N must be a multiple of 256 and K of 64 (-95 otherwise:
+ * the caller keeps its library GEMM for other shapes); any M.
+ * Replaces: the block nn.Linear layers (no bias) of networks/minimal_v4_dit.py -- Attention q/k/v/
+ * output projections (:354-363, :401-404, :432; the DiT runs q|k|v as one fused [3D, D] weight) and
+ * GPT2FeedForward layer1 + exact GELU (:227-254, CP25_EPI_GELU) and layer2. */
+#define CP25_EPI_NONE 0
+#define CP25_EPI_GELU 1
+int cp25_gemm_epi(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int M, int N, int K,
+                  int epilogue, hipStream_t stream);
+
 /* Latents live in "patch layout" [n_tok, 64] fp32, element (tok, p*16 + c), p = p1*2 + p2 (the
  * final layer's "(p1 p2 t C)" order). cp25_patchify builds the x_embedder input rows [n_tok, 72]
  * bf16 (feature c*4 + p): channels 0..15 = gt*mask + x*(1-mask) (gt may be NULL), channel 16 = the

@@ -1,0 +1,12 @@
+set -o pipefail
+export PYTHONUNBUFFERED=1
+mkdir -p gpurun_out
+: > gpurun_out/ab_1w.log
+for i in 1 2; do
+for lib in base nostage; do
+  for k in 1w 2w; do
+    CP25_ATTN_KERNEL=$k timeout -k 10 120 python tools/bench_attn.py --fused --bounded --prescaled --iters 4 --lib tools/lab/libcp25_$lib.so > /tmp/o.txt 2>&1 || exit 1
+    echo "$lib $k $(grep '^{' /tmp/o.txt | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["ms"],2), round(d["tflops"]), d["check_rel_l2"])')" | tee -a gpurun_out/ab_1w.log
+  done
+done
+done
