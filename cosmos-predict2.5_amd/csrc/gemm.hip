@@ -13,14 +13,21 @@
 // Design (MI355X, see DESIGN.md §3 "GEMM"): 256 x 256 output tile per 512-thread workgroup (one per
 // CU), 8 waves as 2 (M) x 4 (N), each wave 128 x 64 with v_mfma_f32_16x16x32_bf16 (32 accumulators,
 // the MFMA shape that holds the higher clock under load, MI355X_MICROARCH "DVFS" item 7); K in 64-deep
-// tiles staged global -> LDS by LDS-DMA (global_load_lds_dwordx4, one 1-KiB piece = 8 rows x 128 B per
-// wave instruction) into two buffers: tile k+1's DMA is in flight while tile k is multiplied. The LDS
+// tiles staged global -> LDS by LDS-DMA (one 1-KiB piece = 8 rows x 128 B per wave instruction). The LDS
 // image is XOR-swizzled on the SOURCE side (16-B chunk c of row r lands at chunk c ^ ((r >> 1) & 7)),
 // which makes every ds_read_b128 fragment read bank-conflict-free. Tiles are walked XCD-aware and
 // grouped (8 row-tiles x all column tiles per group) so the workgroups resident on one XCD share
-// their A and W tiles through that XCD's L2. Rows past M are clamped on load and masked on store.
-// The epilogue stages each wave's bf16 tile through LDS and writes whole 16-B row chunks.
+// their A and W tiles through that XCD's L2.
+//   * gemm_nt_8ph (default, K/64 even): persistent, 8-phase schedule with counted vmcnt across raw barriers
+//     and a pipelined tile seam (below).
+//   * gemm_nt_kernel (odd K/64, or CP25_GEMM_KERNEL=2ph): the round-2 two-phase loop (vmcnt(0) +
+//     __syncthreads per K-tile), one workgroup per tile. Both accumulate in the same order: bit-identical.
 #include "cp25_common.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <type_traits>
 
 #pragma clang fp contract(off)
 
@@ -34,6 +41,12 @@ constexpr int kLds = 2 * kStage;                // two stages: 128 KiB
 constexpr int kGroupM = 8;
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
+
+// one 16-B-per-lane buffer_load ... lds piece (a plain __device__ function: inside the kernel template the host pass
+// drops the kernel's launch stub over this builtin)
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, lds_void_ptr dst, int voffset, int soffset) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, 16, voffset, soffset, 0, 0);
+}
 
 __device__ __forceinline__ float gelu_exact(float a) {
   return 0.5f * a * (1.f + erff(a * 0.70710678118654752440f));  // = cp25_gelu
@@ -150,6 +163,303 @@ gemm_nt_kernel(const unsigned short* __restrict__ A, int64_t lda, const unsigned
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------------------------
+// 8-phase schedule (the default): the same tile, LDS image and MFMA shape, but the K loop is cut into four phases per
+// 64-deep K-tile, one C quadrant (64 x 32 of the wave's 128 x 64) per phase, and the LDS-DMA stream runs 7 half-tiles
+// ahead of the reads (a half-tile = 128 rows x 64 k of one operand, 16 KiB, 2 glds per thread):
+//   * the two wave groups (wr = 0: waves 0-3, wr = 1: waves 4-7; one of each per SIMD) are staggered by one barrier,
+//     so while one issues its quadrant's 16 MFMAs the other issues its LDS reads and its DMA piece;
+//   * each phase: [fragment reads; one half-tile DMA] s_barrier [lgkmcnt(0); 16 MFMA at priority 1] s_barrier;
+//   * quadrant order per K-tile (A half, B half): (0,0) reads B0 + A0, (0,1) reads B1, (1,1) reads A1, (1,0) reads
+//     nothing (B0 kept in registers), so every read of K-tile t happens in its first three phases;
+//   * DMA order per K-tile: B0, A0, B1, A1, issued for K-tile t+2 (same buffer as t) in phases 1-3 of t and phase 0 of
+//     t+1: each half-tile is re-filled >= 2 phases after its last read (B0: 1 phase, its reads retired by the
+//     lgkmcnt(8) before phase 0's first barrier);
+//   * the only VM wait is a counted vmcnt(6) in phase 3 (3 half-tiles stay in flight across every barrier), which
+//     retires K-tile t+1 before the barrier that precedes its first read; raw s_barrier (no __syncthreads, whose
+//     fence would drain the DMA with vmcnt(0)), all LDS in one __shared__ array.
+constexpr int kHalf = 128 * kBK * 2;  // 16 KiB
+constexpr int kBuf8 = 4 * kHalf;      // A0 A1 B0 B1
+
+// Persistent: one workgroup per CU walks tiles my_slot, my_slot + grid, ... (my_slot XCD-remapped). The tile
+// seam is pipelined: after a tile's main loop its C tile is staged through the LDS into registers, then the NEXT
+// tile's K-tiles 0 and 1 are queued (all 8 half-tiles) BEFORE this tile's 16 C stores, so every counted wait that
+// follows can leave the stores in flight (the VM counter retires in order): vmcnt(24) retires the next K-tile 0,
+// vmcnt(6 + 16) at phase 3 of K-tile 0 retires K-tile 1; by phase 3 of K-tile 1 the stores have had two K-tiles
+// to drain. (Issued in the epilogue with a plain vmcnt(0) wait they cost 8-12 % at K = 2048.) A ragged last
+// row-tile masks its stores, so the counts there fall back to vmcnt(0).
+// kLab (A/B only, CP25_GEMM_KERNEL=8ph_lab<n>): bit 0 skips the C staging and stores (accumulators kept live),
+// bit 4 stages C but skips the global stores, bit 6 makes the C stores nontemporal
+// (measured: a CU start stagger and nontemporal stores do not help at K >= 2048; see DESIGN.md §3 "GEMM").
+template <int kEpi, int kLab = 0>
+__global__ void __launch_bounds__(kThreads, 1)
+gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned short* __restrict__ W, int64_t ldw,
+            unsigned short* __restrict__ C, int64_t ldc, int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf8];
+
+  const int mt = (M + kBM - 1) / kBM, nt = N / kBN;
+  const int n_tiles = mt * nt;
+  const int nk = K / kBK;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int my_slot = xcd_remap(blockIdx.x, gridDim.x);
+
+  auto tile_mn = [&](int tile, int& m0, int& n0) __attribute__((always_inline)) {
+    const int group = tile / (kGroupM * nt);
+    const int first_m = group * kGroupM;
+    const int gsize = min(mt - first_m, kGroupM);
+    m0 = (first_m + (tile % (kGroupM * nt)) % gsize) * kBM;
+    n0 = ((tile % (kGroupM * nt)) / gsize) * kBN;
+  };
+
+  // ---- DMA (buffer_load ... lds): wave w fills pieces 2w, 2w+1 (8 rows each) of every half-tile; lane l -> row
+  // l/8 of the piece, LDS chunk l%8, global chunk (l%8) ^ swz(row), swz(row) = (row >> 1) & 7. A's descriptor ends
+  // at row M (a ragged last tile reads zeros there; those rows are not stored); W's per-wave / per-half row offsets
+  // and the K advance ride in the scalar offset.
+  const int prow = lane >> 3, ppos = lane & 7;
+  int a_vo[2][2], w_vo[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int c = ppos ^ ((4 * j + (prow >> 1)) & 7);  // r = (2 wave + j) 8 + prow: (r >> 1) & 7 = (4 j + prow / 2) & 7
+    w_vo[j] = prow * (int)ldw * 2 + c * 16;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) a_vo[h][j] = ((2 * wave + j) * 8 + h * 128 + prow) * (int)lda * 2 + c * 16;
+  }
+  __amdgpu_buffer_rsrc_t a_rsrc, w_rsrc;
+  auto set_tile = [&](int m0, int n0) __attribute__((always_inline)) {
+    a_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (int64_t)m0 * lda), (short)0,
+                                               (int)((int64_t)min(M - m0, kBM) * lda * 2), 0x00020000);
+    w_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(W + (int64_t)n0 * ldw), (short)0, (int)((int64_t)kBN * ldw * 2),
+                                               0x00020000);
+  };
+  // part 0: B half 0, 1: A half 0, 2: B half 1, 3: A half 1 (LDS: A0 @0, A1 @16K, B0 @32K, B1 @48K)
+  auto issue = [&](int part, int kt, int buf) __attribute__((always_inline)) {
+    const int h = part >> 1;
+    const bool is_a = part & 1;
+    char* dst = smem + buf * kBuf8 + (is_a ? 0 : 2 * kHalf) + h * kHalf + wave * 2048;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (is_a)
+        dma16(a_rsrc, (lds_void_ptr)(dst + j * 1024), a_vo[h][j], kt * kBK * 2);
+      else
+        dma16(w_rsrc, (lds_void_ptr)(dst + j * 1024), w_vo[j], ((2 * wave + j) * 8 + h * 128) * (int)ldw * 2 + kt * kBK * 2);
+    }
+  };
+  auto issue_first_two = [&]() __attribute__((always_inline)) {  // K-tiles 0 and 1 of a tile (nk is even)
+#pragma unroll
+    for (int part = 0; part < 4; ++part) issue(part, 0, 0);
+#pragma unroll
+    for (int part = 0; part < 4; ++part) issue(part, 1, 1);
+  };
+
+  const int fr = lane & 15, fg = lane >> 4;
+  const int frag0 = fr * 128 + 16 * ((0 + fg) ^ ((fr >> 1) & 7));  // k-substep 0
+  const int frag1 = fr * 128 + 16 * ((4 + fg) ^ ((fr >> 1) & 7));  // k-substep 1
+  const int a_row = wr * 64 * 128, b_row = wc * 32 * 128;
+
+  typedef float f32x4_t __attribute__((ext_vector_type(4)));
+  f32x4_t acc[2][2][4][2];
+  bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
+  bool stores_pending = false;  // this wave's previous-tile C stores are in flight, queued after K-tiles 0 and 1
+
+  auto phase = [&](auto qc, auto bc, int kt) __attribute__((always_inline)) {
+    constexpr int Q = decltype(qc)::value, BUF = decltype(bc)::value;
+    const char* sbuf = smem + BUF * kBuf8;
+    if constexpr (Q == 0 || Q == 1) {
+      const char* sb = sbuf + 2 * kHalf + Q * kHalf + b_row;
+      auto& fb = Q == 0 ? fb0 : fb1;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        fb[j][0] = *reinterpret_cast<const bf16x8*>(sb + j * 16 * 128 + frag0);
+        fb[j][1] = *reinterpret_cast<const bf16x8*>(sb + j * 16 * 128 + frag1);
+      }
+    }
+    if constexpr (Q == 0) __builtin_amdgcn_sched_barrier(0);
+    if constexpr (Q == 0 || Q == 2) {
+      const char* sa = sbuf + (Q >> 1) * kHalf + a_row;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        fa[i][0] = *reinterpret_cast<const bf16x8*>(sa + i * 16 * 128 + frag0);
+        fa[i][1] = *reinterpret_cast<const bf16x8*>(sa + i * 16 * 128 + frag1);
+      }
+    }
+    // DMA: K-tile kt + 1 part 3 (Q = 0; K-tile 1 was queued whole at the seam) or K-tile kt + 2 part Q - 1
+    if constexpr (Q == 0) {
+      if (kt > 0 && kt + 1 < nk) issue(3, kt + 1, BUF ^ 1);
+    } else {
+      if (kt + 2 < nk) issue(Q - 1, kt + 2, BUF);
+    }
+    if constexpr (Q == 0) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+    if constexpr (Q == 3) {
+      // retire K-tile kt + 1; newer: K-tile kt + 2 parts 0-2 (6) and, at kt = 0, the previous tile's stores (16)
+      if (kt + 2 >= nk)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if (kt == 0 && stores_pending)
+        asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    constexpr int mq = Q >> 1, nq = (Q == 1 || Q == 2);
+    auto& fb = nq ? fb1 : fb0;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[mq][nq][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb[j][s], acc[mq][nq][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  int tile = my_slot;
+  if (tile >= n_tiles) return;
+  int m0, n0;
+  tile_mn(tile, m0, n0);
+  set_tile(m0, n0);
+  issue_first_two();
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // K-tile 0
+  __builtin_amdgcn_s_barrier();
+
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  while (true) {
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+      for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[mq][nq][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger the second wave group by one barrier
+    __builtin_amdgcn_sched_barrier(0);
+    for (int kt = 0; kt < nk; kt += 2) {
+      phase(I0{}, I0{}, kt);
+      phase(I1{}, I0{}, kt);
+      phase(I2{}, I0{}, kt);
+      phase(I3{}, I0{}, kt);
+      phase(I0{}, I1{}, kt + 1);
+      phase(I1{}, I1{}, kt + 1);
+      phase(I2{}, I1{}, kt + 1);
+      phase(I3{}, I1{}, kt + 1);
+    }
+    if (wr == 0) __builtin_amdgcn_s_barrier();
+    // every wave's reads of this tile are done and no DMA is in flight: the LDS becomes the C tile. Raw barriers
+    // (a __syncthreads() fence would also wait for C stores).
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+
+    const int next = tile + gridDim.x;
+    const bool has_next = next < n_tiles;
+    if constexpr (kLab & 1) {
+#pragma unroll
+      for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+        for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(acc[mq][nq][i][j]));
+      if (!has_next) return;
+      tile = next;
+      tile_mn(tile, m0, n0);
+      set_tile(m0, n0);
+      issue_first_two();
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      continue;
+    }
+
+    // ---- C tile -> LDS [256][256] bf16 (row stride 512 B; 16-B chunk ch of row r at ch ^ sw(r), sw(r) =
+    // 2 ((r >> 2) & 3) = 2 fg for this wave's rows, so the four row groups of a fragment write hit distinct banks).
+    // Element (row, col): row = mq 128 + wr 64 + 16 i + 4 fg + r, col = nq 128 + wc 32 + 16 j + fr; the lane part
+    // of the address has two values (j = 0, 1), the rest is an immediate. The bases are laundered per tile so the
+    // compiler does not hoist them out of the tile loop (they would stay live across the K loop).
+    int ez = 0;
+    asm volatile("" : "+v"(ez));
+    unsigned short* const ct = reinterpret_cast<unsigned short*>(smem);
+    unsigned short* stj[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      stj[j] = ct + wr * 64 * 256 + (wc >> 1) * 64 + ez + 4 * fg * 256 +
+               ((((wc & 1) * 4 + 2 * j + (fr >> 3)) ^ (2 * fg)) << 3) + (fr & 7);
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+      for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float y = rbf(acc[mq][nq][i][j][r]);
+              if constexpr (kEpi == CP25_EPI_GELU) y = gelu_exact(y);
+              stj[j][(mq * 128 + 16 * i + r) * 256 + nq * 128] = f2bf(y);
+            }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // thread t reads rows 16 it + t / 32 (it = 0..15), 16-B chunk t % 32 (sw(row) depends on t only)
+    const int ch = tid & 31, r0 = tid >> 5;
+    const unsigned short* rd = ct + ez + r0 * 256 + ((ch ^ (((r0 >> 2) & 3) << 1)) << 3);
+    u32x4 cv[16];
+#pragma unroll
+    for (int it = 0; it < 16; ++it) cv[it] = *reinterpret_cast<const u32x4*>(rd + it * 16 * 256);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // the LDS is free for the next tile's DMA
+
+    unsigned short* crow = C + (int64_t)(m0 + r0) * ldc + n0 + ch * 8;
+    const bool full = m0 + kBM <= M;
+    const int rows_left = M - (m0 + r0);  // rows of C from this lane's first row (ragged last row-tile)
+    if (has_next) {
+      tile = next;
+      tile_mn(tile, m0, n0);
+      set_tile(m0, n0);
+      issue_first_two();
+    }
+    __builtin_amdgcn_sched_barrier(0);  // the DMAs are queued ahead of the stores (the counts above rely on it)
+    if constexpr (!(kLab & 16)) {
+      if (full) {
+        if constexpr ((kLab & 64) != 0) {
+#pragma unroll
+          for (int it = 0; it < 16; ++it)
+            __builtin_nontemporal_store(cv[it], reinterpret_cast<u32x4*>(crow + (int64_t)it * 16 * ldc));
+        } else {
+#pragma unroll
+          for (int it = 0; it < 16; ++it) *reinterpret_cast<u32x4*>(crow + (int64_t)it * 16 * ldc) = cv[it];
+        }
+      } else {
+#pragma unroll
+        for (int it = 0; it < 16; ++it)
+          if (it * 16 < rows_left) *reinterpret_cast<u32x4*>(crow + (int64_t)it * 16 * ldc) = cv[it];
+      }
+    } else {
+#pragma unroll
+      for (int it = 0; it < 16; ++it) asm volatile("" ::"v"(cv[it]));
+    }
+    if (!has_next) return;
+    // retire the next tile's K-tile 0: the stores (16, when all issued) and K-tile 1 (8) may stay in flight
+    stores_pending = full && !(kLab & 16);
+    if (stores_pending)
+      asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+}
 }  // namespace
 
 extern "C" int cp25_gemm_epi(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int M,
@@ -157,20 +467,47 @@ extern "C" int cp25_gemm_epi(const void* a, int64_t lda, const void* w, int64_t 
   if (!a || !w || !c || M <= 0 || N <= 0 || K <= 0) return CP25_ERR_INVAL;
   if (N % kBN != 0 || K % kBK != 0) return CP25_ERR_DTYPE;  // the tiles this kernel is built for
   if (lda < K || ldw < K || ldc < N || (lda % 8) || (ldw % 8) || (ldc % 8)) return CP25_ERR_INVAL;
+  if (lda >= (1 << 22) || ldw >= (1 << 22)) return CP25_ERR_INVAL;  // 32-bit in-tile byte offsets
   if (((uintptr_t)a | (uintptr_t)w | (uintptr_t)c) & 15) return CP25_ERR_INVAL;
   const int64_t nwg = (int64_t)((M + kBM - 1) / kBM) * (N / kBN);
   if (nwg > 0x7fffffff) return CP25_ERR_INVAL;
   const unsigned short* A = (const unsigned short*)a;
   const unsigned short* Wp = (const unsigned short*)w;
   unsigned short* Cp = (unsigned short*)c;
-  if (epilogue == CP25_EPI_NONE)
-    hipLaunchKernelGGL(gemm_nt_kernel<CP25_EPI_NONE>, dim3((unsigned)nwg), dim3(kThreads), 0, stream, A, lda, Wp, ldw,
-                       Cp, ldc, M, N, K);
-  else if (epilogue == CP25_EPI_GELU)
-    hipLaunchKernelGGL(gemm_nt_kernel<CP25_EPI_GELU>, dim3((unsigned)nwg), dim3(kThreads), 0, stream, A, lda, Wp, ldw,
-                       Cp, ldc, M, N, K);
-  else
-    return CP25_ERR_INVAL;
+  if (epilogue != CP25_EPI_NONE && epilogue != CP25_EPI_GELU) return CP25_ERR_INVAL;
+  const char* sel = std::getenv("CP25_GEMM_KERNEL");  // "2ph": the round-2 two-phase loop (A/B only)
+  const bool two_phase = sel && !std::strcmp(sel, "2ph");
+  const bool gelu = epilogue == CP25_EPI_GELU;
+  const dim3 grid((unsigned)nwg), block(kThreads);
+  static int n_cu[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return CP25_ERR_LAUNCH;
+  if (!n_cu[dev] && hipDeviceGetAttribute(&n_cu[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return CP25_ERR_LAUNCH;
+  const int cus = n_cu[dev] >= 8 ? n_cu[dev] & ~7 : n_cu[dev];
+  const dim3 pgrid((unsigned)std::min<int64_t>(nwg, cus));
+  const int lab = sel && !std::strncmp(sel, "8ph_lab", 7) ? std::atoi(sel + 7) : -1;
+  if (lab >= 0 && !gelu && (K / kBK) % 2 == 0) {
+#define CP25_LAB(n)                                                                                            \
+  case n:                                                                                                        \
+    hipLaunchKernelGGL((gemm_nt_8ph<CP25_EPI_NONE, n>), pgrid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K); \
+    break;
+    switch (lab) {
+      CP25_LAB(1) CP25_LAB(16) CP25_LAB(64)
+      default: return CP25_ERR_INVAL;
+    }
+#undef CP25_LAB
+  } else if (two_phase || (K / kBK) % 2 != 0) {
+    if (gelu)
+      hipLaunchKernelGGL(gemm_nt_kernel<CP25_EPI_GELU>, grid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K);
+    else
+      hipLaunchKernelGGL(gemm_nt_kernel<CP25_EPI_NONE>, grid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K);
+  } else {
+    if (gelu)
+      hipLaunchKernelGGL((gemm_nt_8ph<CP25_EPI_GELU, 0>), pgrid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K);
+    else
+      hipLaunchKernelGGL((gemm_nt_8ph<CP25_EPI_NONE, 0>), pgrid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K);
+  }
   CP25_LAUNCH_CHECK();
   return CP25_OK;
 }

@@ -28,16 +28,25 @@ def timed(fn, iters=5):
     return e0.elapsed_time(e1) / iters
 
 
-for name, Nn, K in (("qkv", 6144, 2048), ("proj", 2048, 2048), ("mlp1", 8192, 2048), ("mlp2", 2048, 8192)):
+for name, Nn, K in (("qkv", 6144, 2048), ("proj", 2048, 2048), ("mlp1", 8192, 2048), ("mlp2", 2048, 8192), ("k256", 2048, 256)):
     g = torch.Generator(device=dev).manual_seed(0)
     a = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
     w = (torch.randn(Nn, K, device=dev, generator=g) * K ** -0.5).to(torch.bfloat16)
     out = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
     flop = 2.0 * M * Nn * K
     t_lib = timed(lambda: torch.matmul(a, w.t(), out=out))
+    os.environ["CP25_GEMM_KERNEL"] = "2ph"
+    t_2ph = timed(lambda: N.gemm_epi(a, w, out=out))
+    os.environ["CP25_GEMM_KERNEL"] = "8ph"
     t_own = timed(lambda: N.gemm_epi(a, w, out=out))
-    rec = {"gemm": name, "M": M, "N": Nn, "K": K, "hipblaslt_ms": t_lib, "own_ms": t_own,
-           "hipblaslt_tflops": flop / t_lib / 1e9, "own_tflops": flop / t_own / 1e9}
+    t_lib2 = timed(lambda: torch.matmul(a, w.t(), out=out))
+    labs = {}
+    for lab in [x for x in os.environ.get("GEMM_LABS", "").split(",") if x]:
+        os.environ["CP25_GEMM_KERNEL"] = "8ph_lab" + lab
+        labs[lab] = timed(lambda: N.gemm_epi(a, w, out=out))
+    os.environ["CP25_GEMM_KERNEL"] = "8ph"
+    rec = {"gemm": name, "M": M, "N": Nn, "K": K, "hipblaslt_ms": [t_lib, t_lib2], "own_ms": t_own,
+           "own_2ph_ms": t_2ph, "lab_ms": labs, "hipblaslt_tflops": flop / min(t_lib, t_lib2) / 1e9, "own_tflops": flop / t_own / 1e9}
     if name == "mlp1":
         def unfused():
             torch.matmul(a, w.t(), out=out)
