@@ -46,7 +46,7 @@ _I64 = ctypes.c_int64
 _I = ctypes.c_int
 _F = ctypes.c_float
 
-# symbol -> argtypes (restype is always int)
+# symbol -> argtypes (restype int, except the *_workspace_bytes queries)
 SIGNATURES = {
     "cp25_attn_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, c_int64_p, _F, _P],
     "cp25_attn_fwd_split": [_P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, c_int64_p, _F, _I,
@@ -74,6 +74,9 @@ SIGNATURES = {
                     _I, _I, _I, _I, _I, _I, _P],
     "cp25_rms_norm_silu": [_P, _P, _P, _I64, _I, _I, _P],
     "cp25_softmax_rows": [_P, _I64, _I, _I64, _F, _P, _I64, _P],
+    "cp25_vae_attn": [_P, _I64, _I64, _P, _I64, _I64, _P, _I64, _I64, _P, _I64, _I64, _I, _I, _I, _I, _F, _P, _I64,
+                      _P],
+    "cp25_vae_attn_workspace_bytes": [_I, _I, _I, _I],
 }
 
 
@@ -100,7 +103,8 @@ def load_library() -> ctypes.CDLL:
             raise RuntimeError(f"libcp25.so does not export {name}")
         if argtypes is not None:
             fn.argtypes = argtypes
-        fn.restype = ctypes.c_size_t if name == "cp25_attn_workspace_bytes" else ctypes.c_int
+        fn.restype = {"cp25_attn_workspace_bytes": ctypes.c_size_t,
+                      "cp25_vae_attn_workspace_bytes": ctypes.c_int64}.get(name, ctypes.c_int)
     _lib = lib
     return lib
 
@@ -394,6 +398,31 @@ def rms_norm_silu(x: torch.Tensor, gamma: torch.Tensor, silu: bool = True, out: 
         raise ValueError("rms_norm_silu expects a contiguous channels-last tensor")
     rc = lib.cp25_rms_norm_silu(_ptr(x), _ptr(gamma), _ptr(out), x.numel() // C, C, int(silu), _stream(x.device))
     _check("cp25_rms_norm_silu", rc)
+    return out
+
+
+def vae_attn(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[torch.Tensor] = None,
+             scale: Optional[float] = None) -> torch.Tensor:
+    """Single-head attention per frame for the VAE AttentionBlock (cp25_vae_attn): q [T, Lq, 384], k / v
+    [T, Lk, 384] bf16 views with unit inner stride (e.g. column slices of the to_qkv output) -> out [T, Lq, 384]."""
+    lib = load_library()
+    for n, t in (("q", q), ("k", k), ("v", v)):
+        if t.dtype != torch.bfloat16 or t.dim() != 3 or t.stride(2) != 1 or t.device != q.device:
+            raise ValueError(f"vae_attn: {n} must be a [T, L, D] bf16 view with unit inner stride")
+    T, Lq, D = q.shape
+    if k.shape[0] != T or v.shape[0] != T or k.shape[2] != D or v.shape[2] != D or v.shape[1] != k.shape[1]:
+        raise ValueError("vae_attn: q / k / v shapes disagree")
+    if out is None:
+        out = torch.empty((T, Lq, D), dtype=torch.bfloat16, device=q.device)
+    if out.shape != q.shape or out.dtype != torch.bfloat16 or out.stride(2) != 1:
+        raise ValueError("vae_attn: out must be a [T, Lq, D] bf16 tensor with unit inner stride")
+    sc = D ** -0.5 if scale is None else float(scale)
+    nbytes = lib.cp25_vae_attn_workspace_bytes(T, Lq, k.shape[1], D)
+    ws = torch.empty((max(nbytes, 0) + 3) // 4, dtype=torch.float32, device=q.device) if nbytes > 0 else None
+    rc = lib.cp25_vae_attn(_ptr(q), q.stride(1), q.stride(0), _ptr(k), k.stride(1), k.stride(0), _ptr(v), v.stride(1),
+                           v.stride(0), _ptr(out), out.stride(1), out.stride(0), T, Lq, k.shape[1], D, sc, _ptr(ws),
+                           max(nbytes, 0), _stream(q.device))
+    _check("cp25_vae_attn", rc)
     return out
 
 

@@ -10,9 +10,9 @@ re-laid-out for the GPU:
   kernel (zero frames are NULL), never a concatenated copy;
 * nearest-2x upsampling is fused into the conv's input gather, the upsample3d frame interleave into
   its epilogue, bias + residual adds into the conv epilogue; RMS_norm + SiLU is one HIP kernel.
-The single-head AttentionBlock core (C = 384 at h/8 x w/8) runs as S = Q K^T (library GEMM, fp32
-out), the HIP row softmax (cp25_softmax_rows, bf16 P) and P V (library GEMM); its 1x1 projections and
-norm are the HIP conv / norm kernels.
+The single-head AttentionBlock core (C = 384 at h/8 x w/8) is the flash kernel cp25_vae_attn reading q / k / v
+straight out of the to_qkv output (no score matrix in HBM); its 1x1 projections and norm are the HIP conv /
+norm kernels.
 
 Context parallel decode (set_context_parallel_group): the reference replicates the VAE on every rank;
 here each rank decodes a band of h/N latent rows (8h/N output rows) of every frame. A 3x3 conv needs
@@ -293,22 +293,17 @@ class WanVAE:
         y = N.rms_norm_silu(x, self.gammas[p + ".norm"], silu=False)
         qkv = self.convs[p + ".to_qkv"](_frames(y), T, H, W)  # [T, H, W, 3C]
         qkv = qkv.view(T, H * W, 3 * C)
-        o = torch.empty((T, H * W, C), dtype=BF16, device=self.device)
-        kv_all = None
+        q, k, v = qkv[:, :, :C], qkv[:, :, C:2 * C], qkv[:, :, 2 * C:]
         if self._band is not None:  # K/V of the whole frame: every band's rows, in row order
             group, _, n = self._band
             kv = qkv[:, :, C:].contiguous()
             kv_all = torch.empty((n,) + tuple(kv.shape), dtype=BF16, device=self.device)
             cpx.all_gather_into(kv_all, kv, group)
-        for t in range(T):
-            # F.scaled_dot_product_attention(q, k, v) on bf16 (wan2pt1.py:251-254): fp32 scores of the
-            # bf16 operands (library GEMM), bf16 P from the HIP row softmax, P V with fp32 accumulation
-            q, k, v = qkv[t, :, :C], qkv[t, :, C:2 * C], qkv[t, :, 2 * C:]
-            if kv_all is not None:
-                k = kv_all[:, t, :, :C].reshape(-1, C)
-                v = kv_all[:, t, :, C:].reshape(-1, C)
-            s = torch.mm(q, k.t(), out_dtype=torch.float32)
-            o[t] = torch.mm(N.softmax_rows(s, C ** -0.5), v.contiguous())
+            kv_all = kv_all.permute(1, 0, 2, 3).reshape(T, n * H * W, 2 * C)  # [T, all rows, 2C]
+            k, v = kv_all[:, :, :C], kv_all[:, :, C:]
+        # F.scaled_dot_product_attention(q, k, v) on bf16, one head (wan2pt1.py:251-254): the flash kernel
+        # cp25_vae_attn (fp32 scores, bf16 P), no score matrix in HBM
+        o = N.vae_attn(q, k, v)
         o = o.view(T, H, W, C)
         return self.convs[p + ".proj"](_frames(o), T, H, W, residual=x)
 

@@ -16,6 +16,9 @@
 // MFMA lane so the epilogue writes 4 contiguous channels (8 B) per lane.
 #include "cp25_common.h"
 
+#include <cstdlib>
+#include <cstring>
+
 namespace {
 
 constexpr int kMaxFrames = 24;
@@ -272,6 +275,236 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
   return CP25_OK;
 }
 
+
+// ---------------------------------------------------------------- 3x3 stride-1 conv with an LDS halo tile
+// The 3x3(x3) convs of the ResidualBlocks and the upsample Resample convs (pad 1 left / right; any top / bottom
+// pad, so the row bands of the banded decode take the same kernel and the same summation order). A workgroup
+// (4 waves, one per SIMD) owns a TH x TW output tile (512 pixels: each wave 4 fragments of 32 pixels of a row)
+// x BN = 32 NT output channels, and walks the K dimension in stages of (temporal tap kt, 16 input channels):
+//   * per stage the (TH + 2) x (TW + 2) input halo (16 channels, 32 B per pixel) and the 9 x BN weight rows of
+//     the stage land in LDS by LDS-DMA (global_load_lds_dwordx4, 32 pixels / couts per wave instruction;
+//     padding, rows past Ho and causal zero frames read a zero page), through a 3-deep LDS ring: stage s + 2's
+//     DMA is in flight while stage s is multiplied (counted vmcnt, raw barriers);
+//   * the 9 spatial taps then read shifted windows of the same halo: each input pixel is fetched from global
+//     memory once per (kt, channel chunk) instead of 9 times, and every LDS read is a contiguous 1-KiB wave read
+//     ([pixel][16 ch] and [tap][cout][16 ch] images: conflict-free without a swizzle);
+//   * per stage and wave 9 x 4 x NT MFMAs (v_mfma_f32_32x32x16_bf16) against 9 (4 + NT) fragment reads, so the
+//     LDS read rate stays under the one 1-KiB read per MFMA a SIMD can be fed (the per-tap kernel above reads
+//     1.3 per MFMA and is LDS-bound).
+// Same accumulation order over k = (kt, kh, kw, ci) per output as conv_igemm_kernel except the order of the
+// channel chunks within a tap, so results match it to fp32 rounding.
+__device__ __attribute__((aligned(16))) unsigned int g_zero_page[64];  // 256 B of zeros (static storage)
+
+template <int NT, int TW>
+__global__ void __launch_bounds__(256, 1) conv3x3_halo_kernel(ConvArgs a) {
+  constexpr int BN = 32 * NT;
+  constexpr int TH = 512 / TW;
+  constexpr int HWD = TW + 2, HHT = TH + 2;
+  constexpr int NHP = HWD * HHT;                   // halo pixels
+  constexpr int W_INS = 9 * NT;                    // wave instructions (32 couts x 32 B) per stage
+  // wave instructions (32 pixels x 32 B) for the halo, padded so every wave issues the same count per stage
+  // (the padding instructions copy the zero page into LDS past the halo): the counted vmcnt below needs it
+  constexpr int HALO_INS = ((NHP + 31) / 32 + W_INS + 3) / 4 * 4 - W_INS;
+  constexpr int HALO_BYTES = HALO_INS * 1024;
+  constexpr int STAGE = HALO_BYTES + W_INS * 1024;
+  constexpr int N_INS = HALO_INS + W_INS;
+  constexpr int INS_PER_WAVE = N_INS / 4;
+  constexpr int FPR = TW / 32;                     // fragments per tile row
+  constexpr int NBUF = 3;                          // LDS ring: stage s + 2's DMA in flight while s is multiplied
+  static_assert(N_INS % 4 == 0 && NBUF * STAGE <= 160 * 1024, "halo conv LDS");
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l31 = lane & 31, hl = lane >> 5;
+  const int tiles_w = a.Wo / TW;
+  const int th0 = (blockIdx.x / tiles_w) * TH, tw0 = (blockIdx.x % tiles_w) * TW;
+  const int n0 = blockIdx.y * BN;
+  const int to = blockIdx.z;
+  const int kc = a.Cin / 16;
+  const int nst = a.KT * kc;
+
+  // ---- this lane's DMA sources (stage independent part): instruction i = wave + 4 u
+  //   halo: pixel offset (hi * Win + wi) * Cin + 8 half, or -1 (zero page)
+  //   weights: ((cout * KT) * 9 + tap) * Cin + 8 half, or -1; + kt * 9 * Cin + c16 * 16 per stage
+  const int half = lane & 1, sub = lane >> 1;
+  int src_off[INS_PER_WAVE];
+#pragma unroll
+  for (int u = 0; u < INS_PER_WAVE; ++u) {
+    const int i = wave + 4 * u;
+    int off = -1;  // -1: the zero page
+    if (i < HALO_INS) {
+      const int h = i * 32 + sub;
+      if (h < NHP) {
+        const int hr = h / HWD, hc = h % HWD;
+        const int hu = th0 - a.pad_top + hr, wu = tw0 - a.pad_left + hc;  // (upsampled) input coordinates
+        const int Hs = a.upsample ? 2 * a.Hin : a.Hin, Ws = a.upsample ? 2 * a.Win : a.Win;
+        if (hu >= 0 && hu < Hs && wu >= 0 && wu < Ws) {
+          const int hi = a.upsample ? hu >> 1 : hu, wi = a.upsample ? wu >> 1 : wu;
+          off = (hi * a.Win + wi) * a.Cin + 8 * half;
+        }
+      }
+    } else if (i < N_INS) {
+      const int wi_ = i - HALO_INS;
+      const int tap = wi_ / NT, cb = wi_ % NT;
+      const int co = n0 + cb * 32 + sub;
+      if (co < a.Cout) off = (co * a.KT * 9 + tap) * a.Cin + 8 * half;
+    }
+    src_off[u] = off;
+  }
+  const unsigned short* zero = reinterpret_cast<const unsigned short*>(g_zero_page);
+
+  auto issue = [&](int st, int buf) __attribute__((always_inline)) {
+    const int kt = st / kc, c16 = (st % kc) * 16;
+    const int fi = to * a.stride_t + kt;
+    const unsigned short* fr = fi < a.n_frames ? a.frames[fi] : nullptr;
+    const unsigned short* wst = a.w + kt * 9 * a.Cin + c16;
+    char* base = smem + buf * STAGE;
+#pragma unroll
+    for (int u = 0; u < INS_PER_WAVE; ++u) {
+      const int i = wave + 4 * u;
+      {
+        const unsigned short* src;
+        char* dst;
+        if (i < HALO_INS) {
+          src = (fr != nullptr && src_off[u] >= 0) ? fr + src_off[u] + c16 : zero;
+          dst = base + i * 1024;
+        } else {
+          src = src_off[u] >= 0 ? wst + src_off[u] : zero;
+          dst = base + HALO_BYTES + (i - HALO_INS) * 1024;
+        }
+        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      }
+    }
+  };
+
+  f32x16 acc[4][NT];
+#pragma unroll
+  for (int f = 0; f < 4; ++f)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[f][j][r] = 0.f;
+
+  // fragment f of this wave: tile row (4 wave + f) / FPR, columns ((4 wave + f) % FPR) 32 + [0, 32)
+  int a_base[4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    const int q = wave * 4 + f;
+    a_base[f] = ((q / FPR) * HWD + (q % FPR) * 32 + l31) * 32 + hl * 16;
+  }
+  const int b_base = HALO_BYTES + l31 * 32 + hl * 16;
+
+  // Pipeline: stage s + 2 is queued at the top of stage s (into the buffer stage s - 1 used: every wave passed
+  // the barrier after it); the counted wait at the bottom retires stage s + 1 only (raw barrier: a
+  // __syncthreads() fence would drain the DMA queue).
+  issue(0, 0);
+  if (nst > 1) {
+    issue(1, 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(INS_PER_WAVE) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  int buf = 0;
+  for (int st = 0; st < nst; ++st) {
+    if (st + 2 < nst) issue(st + 2, buf == 0 ? 2 : buf - 1);
+    const char* sb = smem + buf * STAGE;
+    // fragments of tap t + 1 are read while tap t's MFMAs issue (two register sets, order pinned)
+    bf16x8 xa[2][4], wb[2][NT];
+    auto load_tap = [&](int tap, int set) __attribute__((always_inline)) {
+      const int kh = tap / 3, kw = tap % 3;
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        wb[set][j] = *reinterpret_cast<const bf16x8*>(sb + b_base + (tap * BN + j * 32) * 32);
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+        xa[set][f] = *reinterpret_cast<const bf16x8*>(sb + a_base[f] + (kh * HWD + kw) * 32);
+    };
+    load_tap(0, 0);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int cur = tap & 1;
+      if (tap + 1 < 9) load_tap(tap + 1, cur ^ 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[f][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb[cur][j], xa[cur][f], acc[f][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (st + 2 < nst)
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(INS_PER_WAVE) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    buf = buf == NBUF - 1 ? 0 : buf + 1;
+  }
+
+  // ---- epilogue through LDS: bf16(acc + bias) -> [512 px][BN] image (row stride BN * 2 + 8 B: the 8-B writes of
+  // a fragment's 32 pixels hit distinct banks), then 16-B chunks of whole pixel rows to global, + residual
+  constexpr int OST = BN * 2 + 8;
+  static_assert(512 * OST <= NBUF * STAGE, "halo conv epilogue staging");
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    const int px = (wave * 4 + f) * 32 + l31;  // tile pixel (fragment-major = row-major within the tile)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int cl = j * 32 + 8 * g + 4 * hl;
+        u16x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = acc[f][j][4 * g + e];
+          if (a.bias != nullptr && n0 + cl + e < a.Cout) x += bf2f(a.bias[n0 + cl + e]);
+          w[e] = f2bf(x);
+        }
+        *reinterpret_cast<u16x4*>(smem + px * OST + cl * 2) = w;
+      }
+  }
+  __syncthreads();
+  const int M = a.Ho * a.Wo;
+  constexpr int CPP = BN / 8;  // 16-B chunks per pixel
+  const bool vec_ok = (a.Cout % 8) == 0 && n0 + BN <= a.Cout;
+  for (int idx = tid; idx < 512 * CPP; idx += 256) {
+    const int px = idx / CPP, c = idx % CPP;
+    const int q = px >> 5;
+    const int ho = th0 + q / FPR, wo = tw0 + (q % FPR) * 32 + (px & 31);
+    if (ho >= a.Ho) continue;
+    const int64_t o = ((int64_t)to * M + (int64_t)ho * a.Wo + wo) * a.Cout + n0 + c * 8;
+    const u16x8 cv = *reinterpret_cast<const u16x8*>(smem + px * OST + c * 16);
+    if (vec_ok) {
+      u16x8 w = cv;
+      if (a.residual != nullptr) {
+        const u16x8 r = *reinterpret_cast<const u16x8*>(a.residual + o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) w[e] = f2bf(bf2f(cv[e]) + bf2f(r[e]));
+      }
+      *reinterpret_cast<u16x8*>(a.out + o) = w;
+    } else {
+      for (int e = 0; e < 8; ++e) {
+        if (n0 + c * 8 + e >= a.Cout) break;
+        float v = bf2f(cv[e]);
+        if (a.residual != nullptr) v = rbf(v + bf2f(a.residual[o + e]));
+        a.out[o + e] = f2bf(v);
+      }
+    }
+  }
+}
+
+template <int NT, int TW>
+int launch_conv_halo(const ConvArgs& a, hipStream_t s) {
+  constexpr int TH = 512 / TW;
+  dim3 grid((unsigned)(cdiv(a.Ho, TH) * (a.Wo / TW)), (unsigned)cdiv(a.Cout, 32 * NT), (unsigned)a.Tout);
+  hipLaunchKernelGGL((conv3x3_halo_kernel<NT, TW>), grid, dim3(256), 0, s, a);
+  CP25_LAUNCH_CHECK();
+  return CP25_OK;
+}
+
 // ---------------------------------------------------------------- AttentionBlock softmax
 // P = softmax(S * scale) per row, fp32 scores in, bf16 probabilities out (the bf16 operand of the
 // P.V GEMM). One 256-thread workgroup per row: pass 1 keeps a per-thread running (max, sum) over a
@@ -346,6 +579,20 @@ extern "C" int cp25_conv3d(const void* const* frames, int n_frames, const void* 
   a.out_split = out_split;
   a.out_C = out_split > 0 ? out_split : Cout;
   if (a.Ho <= 0 || a.Wo <= 0) return CP25_ERR_INVAL;
+  // 3x3 stride-1 pad-1 convs: the halo kernel (CP25_CONV_KERNEL=tap selects the per-tap kernel, A/B only)
+  const char* sel = std::getenv("CP25_CONV_KERNEL");
+  // (any top / bottom pad: the banded decode passes haloed bands with pads 0 or -1 there)
+  const bool halo_ok = KH == 3 && KW == 3 && stride_hw == 1 && out_split == 0 && pad_left == 1 && pad_right == 1 &&
+                       Cout >= 64 && a.Wo % 32 == 0 &&
+                       (int64_t)Hin * Win * Cin < (1LL << 31) && (int64_t)Cout * KT * 9 * Cin < (1LL << 31) &&
+                       !(sel && !std::strcmp(sel, "tap"));
+  if (halo_ok) {
+    const int tw = a.Wo % 128 == 0 ? 128 : (a.Wo % 64 == 0 ? 64 : 32);
+    // BN = 96 for every Cout (96 / 192 / 384 in the decoder): with BN = 128 the 256 accumulators spill
+    if (tw == 128) return launch_conv_halo<3, 128>(a, stream);
+    if (tw == 64) return launch_conv_halo<3, 64>(a, stream);
+    return launch_conv_halo<3, 32>(a, stream);
+  }
   const int bk = (Cin % 64 == 0) ? 64 : (Cin % 32 == 0 ? 32 : 16);
   int nt;
   if (Cout <= 32) nt = 1;

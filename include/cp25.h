@@ -211,11 +211,24 @@ int cp25_conv3d(const void* const* frames, int n_frames, const void* weight, con
 int cp25_rms_norm_silu(const void* x, const void* gamma, void* y, int64_t n_pix, int C, int do_silu,
                        hipStream_t stream);
 
+/* o = softmax(q k^T * scale) v per frame, one head of D = 384 (the Wan VAE AttentionBlock), bf16 in / out, fp32
+ * scores and sums, bf16 P. q [T][Lq][D], k / v [T][Lk][D], o [T][Lq][D] given as base pointers with row strides
+ * (ld*) and frame strides (f*) in elements (multiples of 8, 16-B aligned bases), so q / k / v can be column
+ * slices of the to_qkv output [T][L][3D]. Flash kernel (no score matrix in HBM): two passes over the keys
+ * (exact row max, then exp / sum / P V). Replaces F.scaled_dot_product_attention in AttentionBlock.forward
+ * (tokenizers/wan2pt1.py:225-261, q, k, v = [b*t, 1, h*w, c]). Returns CP25_ERR_DTYPE for D != 384.
+ * When the query blocks do not cover the GPU the keys are split over several workgroups, whose partials go to
+ * `workspace` (cp25_vae_attn_workspace_bytes(T, Lq, Lk, D) bytes, 16-B aligned; 0 = none needed) and are merged
+ * by a second kernel on the same stream. */
+int64_t cp25_vae_attn_workspace_bytes(int T, int Lq, int Lk, int D);
+int cp25_vae_attn(const void* q, int64_t ldq, int64_t fq, const void* k, int64_t ldk, int64_t fk, const void* v,
+                  int64_t ldv, int64_t fv, void* o, int64_t ldo, int64_t fo, int T, int Lq, int Lk, int D, float scale,
+                  void* workspace, int64_t workspace_bytes, hipStream_t stream);
+
 /* p[r, :] = softmax(s[r, :] * scale) for `rows` rows of `cols` fp32 scores (row stride ld_s elements)
  * -> bf16 probabilities (row stride ld_p); vector loads/stores when rows are 16-B / 8-B aligned. The
- * AttentionBlock core of the VAE (single head, C = 384) runs as S = Q K^T (library GEMM, fp32 out),
- * this kernel, and P V (library GEMM): replaces the softmax inside F.scaled_dot_product_attention in
- * AttentionBlock.forward (wan2pt1.py:234-261). */
+ * round-1 VAE AttentionBlock ran S = Q K^T (library GEMM, fp32 out), this kernel, and P V (library GEMM);
+ * since round 2 it runs cp25_vae_attn and this entry point is kept for the A/B and its tests. */
 int cp25_softmax_rows(const float* s, int64_t rows, int cols, int64_t ld_s, float scale, void* p, int64_t ld_p,
                       hipStream_t stream);
 
