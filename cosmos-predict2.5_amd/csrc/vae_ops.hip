@@ -18,6 +18,7 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 namespace {
 
@@ -293,7 +294,16 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
 //     1.3 per MFMA and is LDS-bound).
 // Same accumulation order over k = (kt, kh, kw, ci) per output as conv_igemm_kernel except the order of the
 // channel chunks within a tap, so results match it to fp32 rounding.
-__device__ __attribute__((aligned(16))) unsigned int g_zero_page[64];  // 256 B of zeros (static storage)
+__device__ __attribute__((aligned(16))) unsigned int g_zero_page[64];
+
+// compile-time loop: f(integral_constant<int, I>) for I = 0 .. N-1, in order
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
+}  // 256 B of zeros (static storage)
 
 template <int NT, int TW>
 __global__ void __launch_bounds__(256, 1) conv3x3_halo_kernel(ConvArgs a) {
@@ -317,17 +327,23 @@ __global__ void __launch_bounds__(256, 1) conv3x3_halo_kernel(ConvArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l31 = lane & 31, hl = lane >> 5;
+  // grid.x = (spatial tile, output frame) with the frame fastest, XCD-remapped: the Tout workgroups of one spatial
+  // tile run together on one XCD and share their input halos (a frame feeds KT output frames) through its L2
   const int tiles_w = a.Wo / TW;
-  const int th0 = (blockIdx.x / tiles_w) * TH, tw0 = (blockIdx.x % tiles_w) * TW;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int to = lin % a.Tout, tile = lin / a.Tout;
+  const int th0 = (tile / tiles_w) * TH, tw0 = (tile % tiles_w) * TW;
   const int n0 = blockIdx.y * BN;
-  const int to = blockIdx.z;
   const int kc = a.Cin / 16;
   const int nst = a.KT * kc;
 
   // ---- this lane's DMA sources (stage independent part): instruction i = wave + 4 u
   //   halo: pixel offset (hi * Win + wi) * Cin + 8 half, or -1 (zero page)
   //   weights: ((cout * KT) * 9 + tap) * Cin + 8 half, or -1; + kt * 9 * Cin + c16 * 16 per stage
-  const int half = lane & 1, sub = lane >> 1;
+  // lane l of a DMA instruction moves 16 B (8 channels) of pixel / cout l % 32, channel half l / 32: the LDS images
+  // are [32-pixel block][half][32][16 B] and [tap][cout block][half][32][16 B], so a fragment read (32 pixels or
+  // couts x one half per 32 lanes) is 512 contiguous bytes: bank-conflict-free
+  const int half = lane >> 5, sub = lane & 31;
   int src_off[INS_PER_WAVE];
 #pragma unroll
   for (int u = 0; u < INS_PER_WAVE; ++u) {
@@ -354,10 +370,18 @@ __global__ void __launch_bounds__(256, 1) conv3x3_halo_kernel(ConvArgs a) {
   }
   const unsigned short* zero = reinterpret_cast<const unsigned short*>(g_zero_page);
 
+  // the (up to 3) input frames of this output frame, read from the kernel arguments once: a dynamically indexed
+  // argument load inside the loop is an SMEM access, and with one in flight the compiler's LDS waits degrade to
+  // lgkmcnt(0)
+  const unsigned short* frk[3];
+#pragma unroll
+  for (int kt = 0; kt < 3; ++kt) {
+    const int fi = to * a.stride_t + kt;
+    frk[kt] = (kt < a.KT && fi < a.n_frames) ? a.frames[fi] : nullptr;
+  }
   auto issue = [&](int st, int buf) __attribute__((always_inline)) {
     const int kt = st / kc, c16 = (st % kc) * 16;
-    const int fi = to * a.stride_t + kt;
-    const unsigned short* fr = fi < a.n_frames ? a.frames[fi] : nullptr;
+    const unsigned short* fr = kt == 0 ? frk[0] : (kt == 1 ? frk[1] : frk[2]);
     const unsigned short* wst = a.w + kt * 9 * a.Cin + c16;
     char* base = smem + buf * STAGE;
 #pragma unroll
@@ -386,14 +410,18 @@ __global__ void __launch_bounds__(256, 1) conv3x3_halo_kernel(ConvArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[f][j][r] = 0.f;
 
-  // fragment f of this wave: tile row (4 wave + f) / FPR, columns ((4 wave + f) % FPR) 32 + [0, 32)
-  int a_base[4];
+  // fragment f of this wave: tile row (4 wave + f) / FPR, columns ((4 wave + f) % FPR) 32 + [0, 32); its halo
+  // pixel for tap (kh, kw) is h = h0[f] + kh HWD + kw, at byte (h / 32) 1024 + hl 512 + (h % 32) 16
+  int h0[4];
 #pragma unroll
   for (int f = 0; f < 4; ++f) {
     const int q = wave * 4 + f;
-    a_base[f] = ((q / FPR) * HWD + (q % FPR) * 32 + l31) * 32 + hl * 16;
+    h0[f] = (q / FPR) * HWD + (q % FPR) * 32 + l31;
   }
-  const int b_base = HALO_BYTES + l31 * 32 + hl * 16;
+  const int b_base = HALO_BYTES + hl * 512 + l31 * 16;
+  static_assert(NT == 3, "the counted LDS waits below assume 3 + 4 fragment reads per tap");
+  typedef __attribute__((address_space(3))) const char* lds_cptr;
+  const unsigned smem_lds = (unsigned)(uintptr_t)(lds_cptr)smem;
 
   // Pipeline: stage s + 2 is queued at the top of stage s (into the buffer stage s - 1 used: every wave passed
   // the barrier after it); the counted wait at the bottom retires stage s + 1 only (raw barrier: a
@@ -410,23 +438,37 @@ __global__ void __launch_bounds__(256, 1) conv3x3_halo_kernel(ConvArgs a) {
   int buf = 0;
   for (int st = 0; st < nst; ++st) {
     if (st + 2 < nst) issue(st + 2, buf == 0 ? 2 : buf - 1);
-    const char* sb = smem + buf * STAGE;
-    // fragments of tap t + 1 are read while tap t's MFMAs issue (two register sets, order pinned)
+    // fragments of tap t + 1 are read (inline asm, 3 B + 4 A reads) while tap t's 12 MFMAs issue, behind a
+    // counted lgkmcnt(7) tied to tap t's registers (the compiler's own waits here were lgkmcnt(0): a full LDS
+    // latency every other tap)
+    const unsigned sbase = smem_lds + buf * STAGE;
+    const unsigned b_addr = sbase + b_base;
     bf16x8 xa[2][4], wb[2][NT];
-    auto load_tap = [&](int tap, int set) __attribute__((always_inline)) {
-      const int kh = tap / 3, kw = tap % 3;
+    auto load_tap = [&](auto TC, bf16x8(&xs)[4], bf16x8(&ws)[NT]) __attribute__((always_inline)) {
+      constexpr int tap = decltype(TC)::value, kh = tap / 3, kw = tap % 3;
 #pragma unroll
       for (int j = 0; j < NT; ++j)
-        wb[set][j] = *reinterpret_cast<const bf16x8*>(sb + b_base + (tap * BN + j * 32) * 32);
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ws[j]) : "v"(b_addr), "i"((tap * NT + j) * 1024));
 #pragma unroll
-      for (int f = 0; f < 4; ++f)
-        xa[set][f] = *reinterpret_cast<const bf16x8*>(sb + a_base[f] + (kh * HWD + kw) * 32);
+      for (int f = 0; f < 4; ++f) {
+        const int h = h0[f] + kh * HWD + kw;
+        const unsigned ad = sbase + (h >> 5) * 1024 + hl * 512 + (h & 31) * 16;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(xs[f]) : "v"(ad));
+      }
     };
-    load_tap(0, 0);
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int cur = tap & 1;
-      if (tap + 1 < 9) load_tap(tap + 1, cur ^ 1);
+    load_tap(std::integral_constant<int, 0>{}, xa[0], wb[0]);
+    static_for<9>([&](auto TC) __attribute__((always_inline)) {
+      constexpr int tap = decltype(TC)::value, cur = tap & 1;
+      if constexpr (tap + 1 < 9) {
+        load_tap(std::integral_constant<int, tap + 1>{}, xa[cur ^ 1], wb[cur ^ 1]);
+        asm volatile("s_waitcnt lgkmcnt(7)"
+                     : "+v"(wb[cur][0]), "+v"(wb[cur][1]), "+v"(wb[cur][2]), "+v"(xa[cur][0]), "+v"(xa[cur][1]),
+                       "+v"(xa[cur][2]), "+v"(xa[cur][3]));
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(wb[cur][0]), "+v"(wb[cur][1]), "+v"(wb[cur][2]), "+v"(xa[cur][0]), "+v"(xa[cur][1]),
+                       "+v"(xa[cur][2]), "+v"(xa[cur][3]));
+      }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int f = 0; f < 4; ++f)
@@ -434,7 +476,7 @@ __global__ void __launch_bounds__(256, 1) conv3x3_halo_kernel(ConvArgs a) {
         for (int j = 0; j < NT; ++j)
           acc[f][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb[cur][j], xa[cur][f], acc[f][j], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
-    }
+    });
     if (st + 2 < nst)
       asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(INS_PER_WAVE) : "memory");
     else
@@ -499,7 +541,7 @@ __global__ void __launch_bounds__(256, 1) conv3x3_halo_kernel(ConvArgs a) {
 template <int NT, int TW>
 int launch_conv_halo(const ConvArgs& a, hipStream_t s) {
   constexpr int TH = 512 / TW;
-  dim3 grid((unsigned)(cdiv(a.Ho, TH) * (a.Wo / TW)), (unsigned)cdiv(a.Cout, 32 * NT), (unsigned)a.Tout);
+  dim3 grid((unsigned)(cdiv(a.Ho, TH) * (a.Wo / TW) * a.Tout), (unsigned)cdiv(a.Cout, 32 * NT), 1u);
   hipLaunchKernelGGL((conv3x3_halo_kernel<NT, TW>), grid, dim3(256), 0, s, a);
   CP25_LAUNCH_CHECK();
   return CP25_OK;
@@ -583,7 +625,7 @@ extern "C" int cp25_conv3d(const void* const* frames, int n_frames, const void* 
   const char* sel = std::getenv("CP25_CONV_KERNEL");
   // (any top / bottom pad: the banded decode passes haloed bands with pads 0 or -1 there)
   const bool halo_ok = KH == 3 && KW == 3 && stride_hw == 1 && out_split == 0 && pad_left == 1 && pad_right == 1 &&
-                       Cout >= 64 && a.Wo % 32 == 0 &&
+                       Cout >= 64 && KT <= 3 && a.Wo % 32 == 0 &&
                        (int64_t)Hin * Win * Cin < (1LL << 31) && (int64_t)Cout * KT * 9 * Cin < (1LL << 31) &&
                        !(sel && !std::strcmp(sel, "tap"));
   if (halo_ok) {
