@@ -229,7 +229,11 @@ class MinimalV1LVGDiT:
         distance to the fp32 truth is unchanged (tests/test_parity_depth_gpu.py holds the HIP path
         within 1.1x of the bf16 reference's own distance); `exact_q_rounding = True` keeps the
         reference's rounding point (q rounded, scale applied to the fp32 scores)."""
-        qb, kb = self.attn_bounds[i]
+        return self._attn_mode(self.attn_bounds[i], hd)
+
+    def _attn_mode(self, bounds, hd: int):
+        """The rule of _self_attn_mode for any RMS-normed q / k pair (also the text cross-attention)."""
+        qb, kb = bounds
         c = hd ** -0.5 * 1.4426950408889634
         if not self.exact_q_rounding and qb * c * kb <= 60.0:
             return c, dict(norm_bounds=(qb * c, kb), prescaled=True)
@@ -531,7 +535,6 @@ class MinimalV1LVGDiT:
         h = N.ln_mod(x, sh, sc, x_st=x_in.stride(0), x_sb=0 if Bx == 1 else x_in.stride(1), **lnk)
         y = None
         gate_prev = None
-        scale_attn = hd ** -0.5
         for i in range(cfg.num_blocks):
             pre = f"blocks.{i}."
             # ---- self attention
@@ -573,10 +576,11 @@ class MinimalV1LVGDiT:
             x = x_new
             # ---- cross attention
             qc = self._linear(_rows(h, n * B), p[pre + "cross_attn.q_proj.weight"], pre + "cross_attn.q_proj")
-            N.head_rmsnorm_rope(qc, n_rows=n * B, B=B, H=H, head_off=0, weight=p[pre + "cross_attn.q_norm.weight"])
+            xq_scale, xattn_kw = self._attn_mode(self.xattn_bounds[i], hd)  # prescaled q as in self-attention
+            N.head_rmsnorm_rope(qc, n_rows=n * B, B=B, H=H, head_off=0, weight=p[pre + "cross_attn.q_norm.weight"],
+                                out_scale=xq_scale)
             o = torch.empty((n, B, D), dtype=BF16, device=self.device)
-            self._cross_attention(qc.view(n, B, H, hd), ctx.k[i], ctx.v[i], o.view(n, B, H, hd), geo, scale_attn,
-                                  self.xattn_bounds[i])
+            self._cross_attention(qc.view(n, B, H, hd), ctx.k[i], ctx.v[i], o.view(n, B, H, hd), geo, xattn_kw)
             y = self._linear(o.view(n * B, D), p[pre + "cross_attn.output_proj.weight"], pre + "cross_attn.output_proj")
             _, _, g_ca = mod(i, 1)
             sh, sc, _ = mod(i, 2)
@@ -601,14 +605,14 @@ class MinimalV1LVGDiT:
         return out.view(n, B, -1)
 
     def _cross_attention(self, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, o: torch.Tensor, geo: Geometry,
-                         scale: float, norm_bounds=None) -> None:
+                         attn_kw: dict) -> None:
         """Text cross-attention of this shard's queries q/o [n, B, H, hd] against k/v [B, Lc, H, hd].
         Multi-view context holds 512 tokens per view and each view's queries see only their own
         (MultiViewCrossAttention, multiview_dit.py:40-55); a shard may span view boundaries."""
         n = q.shape[0]
         n_ctx = k.shape[1] // 512 if k.shape[1] % 512 == 0 else 1
         if geo.n_views == 1 or n_ctx == 1:
-            N.attn_fwd(q.transpose(0, 1), k, v, out=o.transpose(0, 1), softmax_scale=scale, norm_bounds=norm_bounds)
+            N.attn_fwd(q.transpose(0, 1), k, v, out=o.transpose(0, 1), **attn_kw)
             return
         if n_ctx != geo.n_views:
             raise ValueError(f"context has {n_ctx} x 512 tokens for {geo.n_views} views")
@@ -618,8 +622,7 @@ class MinimalV1LVGDiT:
             if a >= b:
                 continue
             ks = slice(vi * 512, (vi + 1) * 512)
-            N.attn_fwd(q[a:b].transpose(0, 1), k[:, ks], v[:, ks], out=o[a:b].transpose(0, 1), softmax_scale=scale,
-                       norm_bounds=norm_bounds)
+            N.attn_fwd(q[a:b].transpose(0, 1), k[:, ks], v[:, ks], out=o[a:b].transpose(0, 1), **attn_kw)
 
     def _cp_self_attention(self, i: int, h: torch.Tensor, o: torch.Tensor, cos, sin, n: int, B: int, cp,
                            cp_size: int, e0=None):
