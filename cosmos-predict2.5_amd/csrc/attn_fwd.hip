@@ -342,10 +342,23 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
     constexpr int par = decltype(PAR)::value;
     constexpr int kb = (par ^ 1) ? kK1 : kK0;  // K(t+1)
     constexpr int vb = par ? kVBuf : 0;         // V(t), relative to V0
+    // lab only (tools/lab/build.sh -DCP25_LAB_QK_HALF / -DCP25_LAB_PV_HALF, wrong results): drop half of the
+    // QK^T (k-steps 4-7) or P.V (k-steps 2-3) MFMAs and their operand reads, the MFMA and LDS work an fp8 operand
+    // (2x MFMA rate, half the bytes) would remove; the softmax VALU is unchanged
+#ifndef CP25_LAB_QK_HALF
+#define CP25_LAB_QK_HALF 0
+#endif
+#ifndef CP25_LAB_PV_HALF
+#define CP25_LAB_PV_HALF 0
+#endif
+    constexpr auto lab_skip = [](int j) constexpr {
+      return (CP25_LAB_QK_HALF && j >= 8 && j < 16) || (CP25_LAB_PV_HALF && j >= 24 && j < 32);
+    };
     bf16x8 ring[5];
     auto issue = [&](auto JC) __attribute__((always_inline)) {
       constexpr int j = decltype(JC)::value;
-      if constexpr (j < 16) {
+      if constexpr (lab_skip(j)) {
+      } else if constexpr (j < 16) {
         constexpr int off = kb + (j & 1) * 32 * kKStride + 32 * (j >> 1);
         asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ring[j % 5]) : "v"(k_rd_lds), "i"(off));
       } else if constexpr (j < 32) {
@@ -358,7 +371,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
         ring[j % 5] = __builtin_bit_cast(bf16x8, r);
       }
     };
-    constexpr auto nreads = [](int j) constexpr { return j < 16 ? 1 : (j < 32 ? 2 : 0); };
+    constexpr auto nreads = [=](int j) constexpr { return lab_skip(j) ? 0 : (j < 16 ? 1 : (j < 32 ? 2 : 0)); };
     // the MFMA-phase wave outranks its softmax partner in issue arbitration (+8% measured)
     __builtin_amdgcn_s_setprio(1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the counted waits below assume an empty LGKM queue
@@ -368,7 +381,8 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
       issue(std::integral_constant<int, j + 4>{});
       constexpr int pending = nreads(j + 1) + nreads(j + 2) + nreads(j + 3) + nreads(j + 4);
       asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(ring[j % 5]) : "i"(pending));
-      if constexpr (j < 16) {
+      if constexpr (lab_skip(j)) {
+      } else if constexpr (j < 16) {
         S[j & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ring[j % 5], qf[j >> 1], j < 2 ? zero16 : S[j & 1], 0, 0, 0);
       } else {
         o[(j - 16) & 3] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ring[j % 5], pb[(j - 16) >> 2], o[(j - 16) & 3], 0, 0, 0);

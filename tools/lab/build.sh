@@ -10,5 +10,5 @@ OBJ=cosmos-predict2.5_amd/cosmos_predict2/_lib/obj
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -fhip-fp32-correctly-rounded-divide-sqrt \
   -fno-honor-nans -fno-slp-vectorize -Iinclude "$@" -c cosmos-predict2.5_amd/csrc/attn_fwd.hip -o /tmp/attn_$name.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tools/lab/libcp25_$name.so /tmp/attn_$name.o \
-  $OBJ/dit_ops.o $OBJ/fp8_ops.o $OBJ/gemm.o $OBJ/unipc.o $OBJ/vae_ops.o
+  $OBJ/dit_ops.o $OBJ/fp8_ops.o $OBJ/gemm.o $OBJ/unipc.o $OBJ/vae_attn.o $OBJ/vae_ops.o
 echo tools/lab/libcp25_$name.so
