@@ -510,10 +510,30 @@ __device__ __forceinline__ void mfma_s_acc(f32x16& d, const bf16x8& k, const bf1
   asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(k), "a"(q));
 }
 constexpr int kLds1w = 3 * kKBuf + 3 * kVBuf;  // 113664
+// kDma (CP25_ATTN_KERNEL=1d): K/V tiles land in LDS by LDS-DMA (buffer_load ... lds) instead of the register
+// staging: no staging VGPRs, no ds_write. The DMA image is lane-linear, so the rows are unpadded (256 B) and
+// XOR-swizzled on the source side: K 16-B chunk c of row r at c ^ (r & 15) (the 16 rows a ds_read_b128 lane
+// group reads at one column land on 16 distinct slots), V 64-B block b of row r at b ^ (r & 3) (the 4 rows of a
+// transposed-read group on 4 distinct quarters). A 4-deep ring per operand lets the DMA run two tiles ahead.
+constexpr int kDRow = 2 * kD;                    // 256 B
+constexpr int kDTile = kKBlk * kDRow;            // 16 KiB
+constexpr int kLds1wDma = 8 * kDTile;            // K slots 0-3, V slots 0-3: 128 KiB
 
-template <int kKind, bool kPre>
+// one 16-B-per-lane LDS-DMA piece, as inline asm: with the builtin the compiler cannot tell the DMA's LDS writes
+// from the ring slots being read and puts an s_waitcnt vmcnt(0) before every LDS read of the loop (draining the
+// two-tile-deep DMA queue); the kernel's own counted vmcnt + barrier order the slots instead
+__device__ __forceinline__ void dma16_lds(__amdgpu_buffer_rsrc_t rsrc, __attribute__((address_space(3))) void* dst,
+                                          int voffset) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)dst);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :
+               : "s"(m0), "v"(voffset), "s"(rsrc)
+               : "memory", "m0");
+}
+
+template <int kKind, bool kPre, bool kDma = false>
 __global__ void __launch_bounds__(kThreads1w, 1) attn_fwd_1w(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[kLds1w];
+  __shared__ __attribute__((aligned(16))) char smem[kDma ? kLds1wDma : kLds1w];
 
   const int nwg = gridDim.x;
   const int tile = xcd_remap(blockIdx.x, nwg);
@@ -575,7 +595,21 @@ __global__ void __launch_bounds__(kThreads1w, 1) attn_fwd_1w(AttnArgs a) {
   const int srow = tid >> 4, sch = tid & 15;
   const int stk_off = (int)(srow * a.k_sl * 2) + sch * 16, stk_step = (int)(16 * a.k_sl * 2);
   const int stv_off = (int)(srow * a.v_sl * 2) + sch * 16, stv_step = (int)(16 * a.v_sl * 2);
-  u32x4 stk[4], stv[4];  // staged K(t+3) / V(t+2), in flight across the iteration's barrier
+  u32x4 stk[4], stv[4];  // staged K(t+3) / V(t+2), in flight across the iteration's barrier (register mode)
+  // DMA mode: wave w fills 1-KiB pieces w + 4u (u < 4) of a tile = rows 4 (w + 4u) + lane / 16; lane l writes
+  // physical chunk l % 16 of its row, so it loads the logical chunk that the swizzle puts there
+  int dk_src[4], dv_src[4];
+  if constexpr (kDma) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int row = 4 * (wave + 4 * u) + (lane >> 4);
+      const int pc = lane & 15;
+      const int lck = pc ^ (row & 15);
+      const int lcv = (((pc >> 2) ^ (row & 3)) << 2) | (pc & 3);
+      dk_src[u] = row * (int)(a.k_sl * 2) + lck * 16;
+      dv_src[u] = row * (int)(a.v_sl * 2) + lcv * 16;
+    }
+  }
   // tile t of K (kv = 0) or V (kv = 1); tiles past the end read as zeros (empty descriptor)
   auto tile_rsrc = [&](int kv, int t) __attribute__((always_inline)) {
     const int64_t sl = kv ? a.v_sl : a.k_sl;
@@ -619,23 +653,47 @@ __global__ void __launch_bounds__(kThreads1w, 1) attn_fwd_1w(AttnArgs a) {
   };
 
   // per-lane LDS read offsets (the slot base is added once per iteration, the rest is immediate)
-  const int k_rd = l31 * kKStride + 16 * hl;
+  constexpr int VSTR = kDma ? kDRow : kVStride;
+  constexpr int KBUF = kDma ? kDTile : kKBuf, VBUF = kDma ? kDTile : kVBuf;
+  constexpr int VBASE = kDma ? 4 * kDTile : 3 * kKBuf;  // V slot 0
+  constexpr int NSLOT = kDma ? 4 : 3;
   const int grp = lane >> 4, gi = lane & 15;
   const int tq = gi >> 2, tp = gi & 3;
-  const int v_rd = 3 * kKBuf + (4 * (grp >> 1) + tq) * kVStride + 32 * (grp & 1) + 8 * tp;
+  // register mode: padded rows, everything but the slot an immediate; DMA mode: the swizzled chunk / block
+  // depends on the lane, so the row base is per lane and the chunk / block offset is added per read
+  const int k_rd = kDma ? l31 * kDRow : l31 * kKStride + 16 * hl;
+  const int v_rd = kDma ? VBASE + (4 * (grp >> 1) + tq) * kDRow + 32 * (grp & 1) + 8 * tp
+                        : 3 * kKBuf + (4 * (grp >> 1) + tq) * kVStride + 32 * (grp & 1) + 8 * tp;
+  const int kx = l31 & 15;  // DMA mode: K row swizzle (row & 15 = l31 & 15 for every 32-row half)
 
   auto k_frag = [&](const char* kb, int kt, int s) __attribute__((always_inline)) {
-    return *reinterpret_cast<const bf16x8*>(kb + kt * 32 * kKStride + 32 * s);
+    if constexpr (kDma) return *reinterpret_cast<const bf16x8*>(kb + kt * 32 * kDRow + 16 * ((2 * s + hl) ^ kx));
+    else return *reinterpret_cast<const bf16x8*>(kb + kt * 32 * kKStride + 32 * s);
   };
   // V^T fragment of k-step ks (16 keys) and d-block db: two transposed 4x16-bit reads
   auto v_frag = [&](const char* vb, int ks, int db) __attribute__((always_inline)) {
     typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-    const int off = 16 * ks * kVStride + 64 * db;
+    const int off = kDma ? 16 * ks * kDRow + 64 * (db ^ tq) : 16 * ks * kVStride + 64 * db;
     const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds_char_ptr)(vb + off));
-    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds_char_ptr)(vb + off + 8 * kVStride));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds_char_ptr)(vb + off + 8 * VSTR));
     typedef short s16x8 __attribute__((ext_vector_type(8)));
     const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     return __builtin_bit_cast(bf16x8, r);
+  };
+  // DMA mode: the four pieces of this wave for tile t of K (kv 0) or V (kv 1) into a slot
+  auto dma_piece = [&](const __amdgpu_buffer_rsrc_t& rs, int kv, int slot, int u, int t) __attribute__((always_inline)) {
+    char* dst = smem + (kv ? VBASE : 0) + slot * kDTile + (wave + 4 * u) * 1024;
+#ifdef CP25_ATTN_DMA_GLOBAL
+    // lab (bench shape only: Lk % 64 == 0): global_load_lds with per-lane addresses instead of the buffer form
+    const char* src = (const char*)(kv ? vp : kp) + (int64_t)min(t, ntiles - 1) * kKBlk * (kv ? a.v_sl : a.k_sl) * 2 +
+                      (kv ? dv_src[u] : dk_src[u]);
+    const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)dst);
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" : : "s"(m0), "v"(src) : "memory", "m0");
+    (void)rs;
+#else
+    (void)t;
+    dma16_lds(rs, (__attribute__((address_space(3))) void*)dst, kv ? dv_src[u] : dk_src[u]);
+#endif
   };
 
   f32x16 S[2][2];     // [half parity][q-block]: S^T of a 32-key half tile
@@ -644,20 +702,44 @@ __global__ void __launch_bounds__(kThreads1w, 1) attn_fwd_1w(AttnArgs a) {
 
   // ---- prologue: K(0), K(1), V(0) -> slots 0, 1, 0; V slot 2 zeroed (V(-1) of the P.V(-1) of
   // sub-step 0, with P = 0); S(0) = QK^T(half 0) ----
-  load_tile(0, 0, stk);
-  write_k(0, stk);
-  load_tile(0, 1, stk);
-  write_k(1, stk);
-  load_tile(1, 0, stv);
-  write_v(0, stv);
-  {
-    const u32x4 z = {0u, 0u, 0u, 0u};
-    const u32x4 zs[4] = {z, z, z, z};
-    write_v(2, zs);
+  if constexpr (kDma) {
+    // K(0), K(1), V(0) -> slots 0, 1, 0; V slot 3 (V(-1)) zeroed; K(2), V(1) in flight into slots 2, 1
+    {
+      const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(smem + VBASE + 3 * kDTile + (tid + 256 * i) * 16) = z;
+    }
+    const auto rk0 = tile_rsrc(0, 0), rk1 = tile_rsrc(0, 1), rv0 = tile_rsrc(1, 0);
+    const auto rk2 = tile_rsrc(0, 2), rv1 = tile_rsrc(1, 1);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) dma_piece(rk0, 0, 0, u, 0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) dma_piece(rk1, 0, 1, u, 1);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) dma_piece(rv0, 1, 0, u, 0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) dma_piece(rk2, 0, 2, u, 2);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) dma_piece(rv1, 1, 1, u, 1);
+    asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  } else {
+    load_tile(0, 0, stk);
+    write_k(0, stk);
+    load_tile(0, 1, stk);
+    write_k(1, stk);
+    load_tile(1, 0, stv);
+    write_v(0, stv);
+    {
+      const u32x4 z = {0u, 0u, 0u, 0u};
+      const u32x4 zs[4] = {z, z, z, z};
+      write_v(2, zs);
+    }
+    load_tile(0, 2, stk);  // written at the top of iteration 0
+    load_tile(1, 1, stv);
+    __syncthreads();
   }
-  load_tile(0, 2, stk);  // written at the top of iteration 0
-  load_tile(1, 1, stv);
-  __syncthreads();
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
     const bf16x8 kf = k_frag(smem + k_rd, 0, s);
@@ -739,11 +821,27 @@ __global__ void __launch_bounds__(kThreads1w, 1) attn_fwd_1w(AttnArgs a) {
   // iteration t: two sub-steps, stage K(t+2) and V(t+1), one barrier; only the last tile can be
   // ragged, so the main loop carries no masking (one basic block for the scheduler)
   auto iteration = [&](auto MASKC, int t, int slot) __attribute__((always_inline)) {
-    const int s1 = slot == 2 ? 0 : slot + 1, s2 = slot == 0 ? 2 : slot - 1;  // (t+1) % 3, (t+2) % 3
-    const char* k_cur = smem + k_rd + slot * kKBuf;
-    const char* k_nxt = smem + k_rd + s1 * kKBuf;
-    const char* v_prv = smem + v_rd + s2 * kVBuf;
-    const char* v_cur = smem + v_rd + slot * kVBuf;
+    // slot = t % NSLOT; s1 = (t+1) % NSLOT, sp = (t-1) % NSLOT (= (t+2) % 3 in register mode)
+    const int s1 = slot == NSLOT - 1 ? 0 : slot + 1, s2 = slot == 0 ? NSLOT - 1 : slot - 1;
+    const char* k_cur = smem + k_rd + slot * KBUF;
+    const char* k_nxt = smem + k_rd + s1 * KBUF;
+    const char* v_prv = smem + v_rd + s2 * VBUF;
+    const char* v_cur = smem + v_rd + slot * VBUF;
+    if constexpr (kDma) {
+      // K(t+3) -> slot (t+3) % 4 = s2 (K(t-1), last read in iteration t-1), V(t+2) -> slot (t+2) % 4 (V(t-2))
+      const int sk3 = s2, sv2 = s1 == NSLOT - 1 ? 0 : s1 + 1;
+      const auto rk = tile_rsrc(0, t + 3);
+      const auto rv = tile_rsrc(1, t + 2);
+      sub_step(std::integral_constant<int, 0>{}, MASKC, 2 * t, k_cur, 1, v_prv, 1, k_nxt, 0, v_cur, 0,
+               [&](int p) { dma_piece(rk, 0, sk3, p, t + 3); });
+      sub_step(std::integral_constant<int, 1>{}, MASKC, 2 * t + 1, k_nxt, 0, v_cur, 0, k_nxt, 1, v_cur, 1,
+               [&](int p) { dma_piece(rv, 1, sv2, p, t + 2); });
+      // K(t+2) and V(t+1) (queued one iteration ago) land before the barrier; this iteration's 8 pieces fly on
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      return s1;
+    }
     // staging, one 16-B piece per MFMA group, spread over the groups in the MFMA shadow (clustered at
     // the iteration start, the 8 loads + 8 LDS writes left the matrix pipe idle for ~500 cycles): piece
     // i of K(t+2) / V(t+1), loaded one iteration ago, goes to LDS, then piece i of K(t+3) / V(t+2) is
@@ -766,19 +864,19 @@ __global__ void __launch_bounds__(kThreads1w, 1) attn_fwd_1w(AttnArgs a) {
     __syncthreads();
     return s1;
   };
-  // carried operands of iteration 0's sub-step 0: K(0) rows 32..63, V(-1) (zeroed slot 2) rows 32..63
+  // carried operands of iteration 0's sub-step 0: K(0) rows 32..63, V(-1) (the zeroed slot) rows 32..63
 #pragma unroll
   for (int g = 0; g < 4; ++g) ck[g] = k_frag(smem + k_rd, 1, g);
-  cv[0] = v_frag(smem + v_rd + 2 * kVBuf, 2, 0);
-  cv[1] = v_frag(smem + v_rd + 2 * kVBuf, 2, 1);
+  cv[0] = v_frag(smem + v_rd + (NSLOT - 1) * VBUF, 2, 0);
+  cv[1] = v_frag(smem + v_rd + (NSLOT - 1) * VBUF, 2, 1);
   int slot = 0;  // t % 3
   for (int t = 0; t < ntiles - 1; ++t) slot = iteration(std::false_type{}, t, slot);
   iteration(std::true_type{}, ntiles - 1, slot);
 
   // ---- drain: P.V(2 ntiles - 1) = V(ntiles - 1) rows 32..63 with P[1] ----
   {
-    const int sl = (ntiles - 1) % 3;
-    const char* vb = smem + v_rd + sl * kVBuf;
+    const int sl = (ntiles - 1) % NSLOT;
+    const char* vb = smem + v_rd + sl * VBUF;
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
       const bf16x8 vf = v_frag(vb, 2 + (g >> 2), g & 3);
@@ -865,14 +963,19 @@ int g_num_cus = 0;
 // then the staging spread over the MFMA groups and carried LDS operands); 1w holds ~1.94 GHz with the
 // MFMA pipe busy 62 % of cycles, 2w ~1.62 GHz at 78 %. Without any K/V staging the 1w loop runs
 // 121-134 ms: what is left is hiding the global loads without a second wave. Read once.
+// CP25_ATTN_KERNEL=1d: the one-wave-per-SIMD kernel with LDS-DMA staging (attn_fwd_1w<.., kDma>): 147.8 ms vs
+// 2w 146.9 and register-staged 1w 151.2 (same box, prescaled, metric shape); PMC: 1.82 GHz at 69 % MFMA busy
+// (2w: 1.62 GHz at 78 %), 50 GB of HBM reads per launch (2w: 27 GB). With the DMA as a compiler builtin the
+// loop got an s_waitcnt vmcnt(0) before every LDS read and ran 430 ms.
 int g_use_1w = -1;
-bool use_1w() {
+int attn_variant() {  // 0: 2w, 1: 1w, 2: 1w + DMA staging
   if (g_use_1w < 0) {
     const char* e = getenv("CP25_ATTN_KERNEL");
-    g_use_1w = (e && e[0] == '1') ? 1 : 0;
+    g_use_1w = (e && e[0] == '1') ? (e[1] == 'd' ? 2 : 1) : 0;
   }
-  return g_use_1w == 1;
+  return g_use_1w;
 }
+bool use_1w() { return attn_variant() != 0; }
 
 int num_cus() {
   if (g_num_cus == 0) {
@@ -971,8 +1074,11 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
   const int64_t nwg = (int64_t)a.nqb * B * H * n_split;
   if (nwg > 0x7fffffff) return CP25_ERR_INVAL;
   if ((prescaled || fixed) && use_1w()) {
-    auto kernel = prescaled ? (Lk <= 4096 ? attn_fwd_1w<1, true> : attn_fwd_1w<0, true>)
-                            : (Lk <= 4096 ? attn_fwd_1w<1, false> : attn_fwd_1w<0, false>);
+    const bool dma = attn_variant() == 2;
+    auto kernel = dma ? (prescaled ? (Lk <= 4096 ? attn_fwd_1w<1, true, true> : attn_fwd_1w<0, true, true>)
+                                   : (Lk <= 4096 ? attn_fwd_1w<1, false, true> : attn_fwd_1w<0, false, true>))
+                      : (prescaled ? (Lk <= 4096 ? attn_fwd_1w<1, true> : attn_fwd_1w<0, true>)
+                                   : (Lk <= 4096 ? attn_fwd_1w<1, false> : attn_fwd_1w<0, false>));
     hipLaunchKernelGGL(kernel, dim3((unsigned)nwg), dim3(kThreads1w), 0, stream, a);
   } else {
     auto kernel = prescaled ? (Lk <= 4096 ? attn_fwd_d128<1, true, true> : attn_fwd_d128<0, true, true>)
