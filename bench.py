@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--resolution", default="704,1280")
     ap.add_argument("--linear-precision", default="bf16", choices=("bf16", "fp8"),
                     help="fp8: the DiT block projections/MLP as fp8 MFMA GEMMs (config 5's option; not the metric)")
+    ap.add_argument("--attention-precision", default="bf16", choices=("bf16", "fp8"),
+                    help="fp8: self-attention Q K^T on e4m3 operands (config 5's option; not the metric)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--backend", default="nccl", help="process-group backend for N > 1 (nccl = RCCL; gloo only "
@@ -120,7 +122,7 @@ def main():
     h, w = (int(x) for x in a.resolution.split(","))
     state_t = 1 + (a.frames - 1) // 4
     pipe = Video2WorldInference(a.model, context_parallel_size=world, device=dev, state_t=state_t,
-                                linear_precision=a.linear_precision)
+                                linear_precision=a.linear_precision, attention_precision=a.attention_precision)
     model = pipe.model
     karras = model.config.use_kerras_sigma_at_inference
     frames = model.tokenizer.get_pixel_num_frames(state_t)
@@ -185,7 +187,7 @@ def main():
 
     if rank == 0:
         valid = (a.num_steps == 35 and a.frames == 121 and (h, w) == (704, 1280) and a.model == "2B/post-trained"
-                 and a.linear_precision == "bf16")
+                 and a.linear_precision == "bf16" and a.attention_precision == "bf16")
         # HBM bytes per self-attention launch: a static prior from the committed rocprofv3 PMC passes of
         # this kernel at this shape (tools/pmc_attn.sh; FETCH_SIZE x2 gfx950 correction + WRITE_SIZE),
         # not collected in this run; only the CP = 1 metric shape was measured, other shapes report null
@@ -205,7 +207,10 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "bf16" if a.linear_precision == "bf16" else "fp8 (block GEMMs) + bf16",
+            "dtype": "bf16" if (a.linear_precision, a.attention_precision) == ("bf16", "bf16") else
+                     " + ".join(x for x, on in (("fp8 (block GEMMs)", a.linear_precision == "fp8"),
+                                                ("fp8 (attention Q K^T)", a.attention_precision == "fp8")) if on)
+                     + " + bf16",
             "data": "synthetic: seeded random 2B/VAE weights, random conditioning image, N(0,1) text embeddings",
             "config": {
                 "workload": f"Predict2.5-2B Image2World {h}x{w}x{frames}f ({a.model}), {a.num_steps} "
@@ -222,11 +227,13 @@ def main():
                 "global_batch": 1,
                 "parallelism": f"cp{world}",
                 "linear_precision": a.linear_precision,
+                "attention_precision": a.attention_precision,
                 "metric_config": valid,
             },
             "roofline": {
                 "bound": "mfma",
-                "kernel": "cp25_attn_fwd (DiT self-attention, bf16 MFMA)",
+                "kernel": "cp25_attn_fwd (DiT self-attention, bf16 MFMA)" if a.attention_precision == "bf16" else
+                          "cp25_attn_fwd_prescaled_fp8qk (DiT self-attention, fp8 Q K^T + bf16 P V MFMA)",
                 "achieved": achieved,
                 "peak": BF16_DENSE_PEAK_TFLOPS,
                 "unit": "TFLOP/s",

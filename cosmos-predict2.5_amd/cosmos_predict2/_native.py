@@ -55,6 +55,9 @@ SIGNATURES = {
                               _F, _I, _P, ctypes.c_size_t, _P],
     "cp25_attn_fwd_prescaled": [_P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, c_int64_p, _F,
                                 _F, _I, _P, ctypes.c_size_t, _P],
+    "cp25_attn_fwd_prescaled_fp8qk": [_P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, c_int64_p, _F,
+                                _F, _I, _P, ctypes.c_size_t, _P],
+    "cp25_cast_fp8_e4m3": [_P, _I64, _P, _I64, _I64, _I64, _F, _P],
     "cp25_attn_workspace_bytes": [_I, _I, _I, _I],
     "cp25_attn_plan": [_I, _I, _I, _I, _I],
     "cp25_ln_mod": [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _P, _P, _I64, _I, _I, _I64, _I64, _F, _P],
@@ -147,14 +150,18 @@ def attn_plan(B: int, H: int, Lq: int, Lk: int, D: int = 128) -> int:
 
 def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[torch.Tensor] = None,
              softmax_scale: Optional[float] = None, n_split: Optional[int] = None,
-             norm_bounds: Optional[Tuple[float, float]] = None, prescaled: bool = False) -> torch.Tensor:
+             norm_bounds: Optional[Tuple[float, float]] = None, prescaled: bool = False,
+             fp8_qk: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
     """softmax(q k^T * scale) v for q [B, Lq, H, 128], k/v [B, Lk, H, 128] (bf16, any strides with
     a contiguous head dim). Returns [B, Lq, H, 128] bf16. n_split: key-range split (None = the
     library's plan for this shape; the fp32 partials live in a caching-allocator workspace).
     norm_bounds: (max |q|, max |k|) upper bounds over all rows, enabling the bounded-shift softmax
     where they are small enough (cp25_attn_fwd_bounded; None = online max only).
     prescaled=True: q rows already carry scale * log2(e) (head_rmsnorm_rope(out_scale=...)), norm_bounds
-    are those of the scaled q and of k with product <= 60 (cp25_attn_fwd_prescaled; softmax_scale unused)."""
+    are those of the scaled q and of k with product <= 60 (cp25_attn_fwd_prescaled; softmax_scale unused).
+    fp8_qk=(q8, k8): with prescaled, Q K^T runs on the e4m3 copies (uint8 views shaped like q / k, from
+    cast_fp8(q * 2^s), cast_fp8(k * 2^-s); cp25_attn_fwd_prescaled_fp8qk); q / k are then only shape
+    references."""
     lib = load_library()
     if q.dtype != torch.bfloat16 or k.dtype != torch.bfloat16 or v.dtype != torch.bfloat16:
         raise ValueError("attn_fwd expects bf16 q/k/v (attention() recasts to bf16 first)")
@@ -180,6 +187,18 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
     if prescaled:
         if qb * kb > 60.0 or qb <= 0.0 or kb <= 0.0:
             raise ValueError(f"prescaled attention needs norm bounds with product <= 60, got {norm_bounds}")
+        if fp8_qk is not None:
+            q8, k8 = fp8_qk
+            if q8.dtype != torch.uint8 or k8.dtype != torch.uint8 or q8.shape != q.shape or k8.shape != k.shape:
+                raise ValueError("fp8_qk: uint8 (e4m3 bit pattern) views shaped like q and k expected")
+            if q8.stride(3) != 1 or k8.stride(3) != 1:
+                raise ValueError("fp8_qk: head dim must be contiguous")
+            strides[0] = _i64x3((q8.stride(0), q8.stride(1), q8.stride(2)))
+            strides[1] = _i64x3((k8.stride(0), k8.stride(1), k8.stride(2)))
+            rc = lib.cp25_attn_fwd_prescaled_fp8qk(_ptr(q8), _ptr(k8), _ptr(v), _ptr(out), B, H, Lq, Lk, D, *strides,
+                                                   qb, kb, int(n_split), _ptr(ws), ws_bytes, _stream(q.device))
+            _check("cp25_attn_fwd_prescaled_fp8qk", rc)
+            return out
         rc = lib.cp25_attn_fwd_prescaled(_ptr(q), _ptr(k), _ptr(v), _ptr(out), B, H, Lq, Lk, D, *strides, qb, kb,
                                          int(n_split), _ptr(ws), ws_bytes, _stream(q.device))
         _check("cp25_attn_fwd_prescaled", rc)
@@ -193,6 +212,23 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
         scale, qb, kb, int(n_split), _ptr(ws), ws_bytes, _stream(q.device),
     )
     _check("cp25_attn_fwd_bounded", rc)
+    return out
+
+
+def cast_fp8(src: torch.Tensor, scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """e4m3(bf16 src * scale) as uint8 bit patterns, row by row over the last dim (cp25_cast_fp8_e4m3); src is a
+    2-D bf16 view with unit inner stride (e.g. the q or k columns of the fused qkv buffer)."""
+    lib = load_library()
+    if src.dtype != torch.bfloat16 or src.dim() != 2 or src.stride(1) != 1:
+        raise ValueError("cast_fp8 expects a 2-D bf16 view with a contiguous last dim")
+    n, w = src.shape
+    if out is None:
+        out = torch.empty((n, w), dtype=torch.uint8, device=src.device)
+    if out.dtype != torch.uint8 or out.shape != src.shape or out.stride(1) != 1:
+        raise ValueError("cast_fp8: out must be a uint8 tensor shaped like src")
+    rc = lib.cp25_cast_fp8_e4m3(_ptr(src), src.stride(0), _ptr(out), out.stride(0), n, w, float(scale),
+                                _stream(src.device))
+    _check("cp25_cast_fp8_e4m3", rc)
     return out
 
 

@@ -207,6 +207,8 @@ class MinimalV1LVGDiT:
         # True: self-attention q rounded to bf16 exactly where the reference rounds it (the scale goes
         # on the fp32 scores); False (default): q * scale * log2(e) rounded once (see _self_attn_mode)
         self.exact_q_rounding = False
+        # "bf16" (default) or "fp8": self-attention Q K^T on e4m3 copies of q and k (set_attention_precision)
+        self.attention_precision = "bf16"
 
     def set_linear_precision(self, precision: str) -> None:
         """"bf16" (default, the reference's arithmetic) or "fp8": the 28 blocks' q/k/v, output, cross-q,
@@ -219,6 +221,25 @@ class MinimalV1LVGDiT:
             raise ValueError(f"linear precision must be 'bf16' or 'fp8', got {precision!r}")
         self.linear_precision = precision
         self._fp8_w = {}
+
+    def set_attention_precision(self, precision: str) -> None:
+        """"bf16" (default, the reference's arithmetic) or "fp8": where the prescaled form applies, the
+        self-attention's Q K^T runs on v_mfma_f32_32x32x64_f8f6f4 over e4m3 copies of q * 4 and k / 4
+        (cp25_cast_fp8_e4m3, power-of-two scales that cancel in the scores; cp25_attn_fwd_prescaled_fp8qk),
+        P and V stay bf16, the softmax fp32. -18 % on the kernel; e4m3's 3 mantissa bits put ~5 % noise on
+        each score, stated in tests/test_attn_fp8qk_gpu.py. No reference counterpart (config 5's option)."""
+        if precision not in ("bf16", "fp8"):
+            raise ValueError(f"attention precision must be 'bf16' or 'fp8', got {precision!r}")
+        self.attention_precision = precision
+
+    def _fp8_qk(self, q_cols: torch.Tensor, k_cols: torch.Tensor, B: int, H: int, hd: int, attn_kw: dict):
+        """attn_fwd kwargs for the fp8 Q K^T form: e4m3 [n, B, H, hd] copies of the q / k columns (2-D row
+        views of the token-major qkv / gathered kv buffers), transposed like the bf16 views."""
+        if self.attention_precision != "fp8" or not attn_kw.get("prescaled"):
+            return attn_kw
+        q8 = N.cast_fp8(q_cols, 4.0).view(-1, B, H, hd).transpose(0, 1)
+        k8 = N.cast_fp8(k_cols, 0.25).view(-1, B, H, hd).transpose(0, 1)
+        return dict(attn_kw, fp8_qk=(q8, k8))
 
     def _self_attn_mode(self, i: int, hd: int):
         """(q out_scale, attn_fwd kwargs) of block i's self-attention. When the norm bound allows
@@ -552,6 +573,7 @@ class MinimalV1LVGDiT:
                 q = qkv.view(n, B, 3 * D)[:, :, :D].view(n, B, H, hd).transpose(0, 1)
                 kk = qkv.view(n, B, 3 * D)[:, :, D:2 * D].view(n, B, H, hd).transpose(0, 1)
                 vv = qkv.view(n, B, 3 * D)[:, :, 2 * D:].view(n, B, H, hd).transpose(0, 1)
+                attn_kw = self._fp8_qk(qkv[:, :D], qkv[:, D:2 * D], B, H, hd, attn_kw)
                 if ev is not None:
                     ev[0].record()
                 N.attn_fwd(q, kk, vv, out=o.view(n, B, H, hd).transpose(0, 1), **attn_kw)
@@ -646,6 +668,7 @@ class MinimalV1LVGDiT:
         N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=0, weight=p[pre + "self_attn.q_norm.weight"],
                             cos=cos, sin=sin, out_scale=q_scale)
         work.wait()
+        attn_kw = self._fp8_qk(qkv[:, :D], kv_all[:, :D], B, H, hd, attn_kw)
         if e0 is not None:
             e0.record()
         kc, vc = kv_chunk_views(kv_all, cp_size * n, B, H, hd)

@@ -107,9 +107,10 @@ class Video2WorldInference:
                  tokenizer_path: Optional[str] = None, context_parallel_size: int = 1, device=None,
                  state_t: Optional[int] = None, text_encoder: Optional[Callable] = None,
                  net_cfg: Optional[DiTConfig] = None, sampler_cfg: Optional[SamplerConfig] = None,
-                 weights_seed: int = 0, linear_precision: str = "bf16"):
+                 weights_seed: int = 0, linear_precision: str = "bf16", attention_precision: str = "bf16"):
         """linear_precision: "bf16" (the reference's arithmetic) or "fp8" (the DiT block GEMMs as fp8
-        MFMA, config 5's option; MinimalV1LVGDiT.set_linear_precision)."""
+        MFMA, config 5's option; MinimalV1LVGDiT.set_linear_precision). attention_precision: "bf16" or
+        "fp8" (self-attention Q K^T on e4m3 operands; MinimalV1LVGDiT.set_attention_precision)."""
         if device is None:
             device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
         self.device = torch.device(device)
@@ -141,6 +142,7 @@ class Video2WorldInference:
         self.model.load_state_dict(sd)
         del sd
         self.model.net.set_linear_precision(linear_precision)
+        self.model.net.set_attention_precision(attention_precision)
         if self.process_group is not None:
             self.model.set_context_parallel_group(self.process_group)
         emb_dim = ncfg.crossattn_proj_in_channels if ncfg.use_crossattn_projection else ncfg.crossattn_emb_channels

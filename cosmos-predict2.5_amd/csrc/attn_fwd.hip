@@ -127,9 +127,18 @@ struct AttnArgs {
 // V(t-1) (last read in 2t-1).
 // kKind 0: self-attention, 1: cross-attention (separate symbols in profiles); kFixed: bounded shift;
 // kPre: q pre-scaled by scale * log2(e) and |q| |k| <= kTop (host-checked): P = exp2(S), shift 0
-template <int kKind, bool kFixed, bool kPre = false>
+// kF8 (cp25_attn_fwd_prescaled_fp8qk, the config-5 fp8 option): q and k arrive as OCP e4m3 (bytes, strides in
+// bytes) and S^T = K Q^T runs on v_mfma_f32_32x32x64_f8f6f4: 4 MFMAs of 64 k per tile instead of 16 of 16,
+// K tiles of 64 rows x 128 B (LDS rows 144 B). P and V stay bf16. The operand k order only has to agree between
+// A and B: lane half h, byte i of both operands is d = 64 s + 32 h + i.
+template <int kKind, bool kFixed, bool kPre = false, bool kF8 = false>
 __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
+  static_assert(!kF8 || kPre, "the fp8 Q K^T form is the prescaled one");
+  constexpr int KSTR = kF8 ? 144 : kKStride;        // K LDS row stride
+  constexpr int KB1 = kKBlk * KSTR;                 // K buffer 1
+  constexpr int VB0 = 2 * kKBlk * KSTR, VB1 = VB0 + kVBuf;
+  typedef int i32x8 __attribute__((ext_vector_type(8)));
 
   const int nwg = gridDim.x;
   const int tile = xcd_remap(blockIdx.x, nwg);
@@ -148,18 +157,28 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   const int hl = lane >> 5;  // lane half
   const bool group_b = __builtin_amdgcn_readfirstlane(tid) >= kThreads / 2;
 
-  const unsigned short* qp = a.q + b * a.q_sb + h * a.q_sh;
-  const unsigned short* kp = a.k + b * a.k_sb + h * a.k_sh + (int64_t)key0 * a.k_sl;
+  constexpr int QKE = kF8 ? 1 : 2;  // bytes per q / k element
+  const char* qp = (const char*)a.q + (b * a.q_sb + h * a.q_sh) * QKE;
+  const char* kp = (const char*)a.k + (b * a.k_sb + h * a.k_sh + (int64_t)key0 * a.k_sl) * QKE;
   const unsigned short* vp = a.v + b * a.v_sb + h * a.v_sh + (int64_t)key0 * a.v_sl;
 
   // ---- Q fragments (B operand of S^T = K Q^T): Q[q][16s + 8hl .. +7], s = 0..7 ----
   const int q_row = qb * kQBlk + wave * kQRows + l31;
   const int q_row_c = q_row < a.Lq ? q_row : a.Lq - 1;
   bf16x8 qf[8];
-  {
-    const unsigned short* src = qp + (int64_t)q_row_c * a.q_sl + 8 * hl;
+  i32x8 qf8[2];
+  if constexpr (kF8) {
+    const char* src = qp + (int64_t)q_row_c * a.q_sl + 32 * hl;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(src + 16 * s);
+    for (int s = 0; s < 2; ++s) {
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(src + 64 * s);
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(src + 64 * s + 16);
+      qf8[s] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+  } else {
+    const char* src = qp + ((int64_t)q_row_c * a.q_sl + 8 * hl) * 2;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(src + 32 * s);
   }
 
   f32x16 o[4];
@@ -191,39 +210,49 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   // chunk u%16. buffer_load: the tile base is a wave-uniform descriptor (SALU only), the per-lane
   // offset is loop-invariant, rows past Lk fall outside the descriptor's range and read as zero
   // (their scores are masked to -inf).
+  // kF8: a K tile is 64 rows x 128 B, 2 chunks of 16 B per thread of group B (rows u/8 + 32 i, chunk u%8)
   const int u = tid & (kThreads / 2 - 1);
-  const int srow = u >> 4, sch = u & 15;
+  const bool kf8 = kF8 && group_b;
+  const int srow = kf8 ? u >> 3 : u >> 4, sch = kf8 ? u & 7 : u & 15;
   const int64_t sl = group_b ? a.k_sl : a.v_sl;
-  const unsigned short* sbase = group_b ? kp : vp;
-  const int st_off = (int)(srow * sl * 2) + sch * 16, st_step = (int)(16 * sl * 2);
+  const int esz = kf8 ? 1 : 2;
+  const char* sbase = group_b ? kp : (const char*)vp;
+  const int st_off = (int)(srow * sl * esz) + sch * 16, st_step = (int)((kf8 ? 32 : 16) * sl * esz);
+  const int nst = kf8 ? 2 : 4;
   u32x4 st[4];
   auto load_tile = [&](int t) __attribute__((always_inline)) {
     const int rows = min(Lk - t * kKBlk, kKBlk);
-    const int nbytes = rows > 0 ? (int)((rows - 1) * sl * 2) + 2 * kD : 0;
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(sbase + (int64_t)t * kKBlk * sl), (short)0, nbytes,
-                                                        0x00020000);
+    const int nbytes = rows > 0 ? (int)((rows - 1) * sl * esz) + esz * kD : 0;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(sbase + (int64_t)t * kKBlk * sl * esz), (short)0,
+                                                        nbytes, 0x00020000);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      st[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, st_off + i * st_step, 0, 0));
+      if (i < nst)
+        st[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, st_off + i * st_step, 0, 0));
   };
-  char* const k_wr = smem + srow * kKStride + sch * 16;
+  char* const k_wr = smem + srow * KSTR + sch * 16;
   char* const v_wr = smem + srow * kVStride + sch * 16;
   auto write_k = [&](auto BUF) __attribute__((always_inline)) {
-    constexpr int kb = decltype(BUF)::value ? kK1 : kK0;
+    constexpr int kb = decltype(BUF)::value ? KB1 : 0;
+    if constexpr (kF8) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(k_wr + kb + 16 * i * kKStride) = st[i];
+      for (int i = 0; i < 2; ++i) *reinterpret_cast<u32x4*>(k_wr + kb + 32 * i * KSTR) = st[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(k_wr + kb + 16 * i * KSTR) = st[i];
+    }
   };
   auto write_v = [&](auto BUF) __attribute__((always_inline)) {
-    constexpr int vb = decltype(BUF)::value ? kV1 : kV0;
+    constexpr int vb = decltype(BUF)::value ? VB1 : VB0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(v_wr + vb + 16 * i * kVStride) = st[i];
   };
 
   // per-lane LDS read bases (everything else is an immediate offset)
-  const char* const k_rd = smem + l31 * kKStride + 16 * hl;  // + kt*32 rows + 32 s bytes
+  const char* const k_rd = smem + l31 * KSTR + (kF8 ? 32 : 16) * hl;  // + kt*32 rows + (64 | 32) s bytes
   const int grp = lane >> 4, gi = lane & 15;
   const int tq = gi >> 2, tp = gi & 3;
-  const char* const v_rd = smem + kV0 + (4 * (grp >> 1) + tq) * kVStride + 32 * (grp & 1) + 8 * tp;  // + rows, + 64 db
+  const char* const v_rd = smem + VB0 + (4 * (grp >> 1) + tq) * kVStride + 32 * (grp & 1) + 8 * tp;  // + rows, + 64 db
   // the same bases as 32-bit LDS addresses for the MFMA phase's asm reads (all offsets < 64 KiB)
   const unsigned k_rd_lds = (unsigned)(uintptr_t)(lds_char_ptr)k_rd;
   const unsigned v_rd_lds = (unsigned)(uintptr_t)(lds_char_ptr)v_rd;
@@ -236,13 +265,28 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   const f32x16 zero16 = {};
 
   // S^T = K Q^T on the K buffer; the first MFMA of each chain takes an inline-constant zero C
+  // fp8 form: one A fragment = 32 B of a K row (d 64 s + 32 hl ..), two ds_read_b128
+  auto k_frag8 = [&](int kb, int kt, int s) __attribute__((always_inline)) {
+    const u32x4 lo = *reinterpret_cast<const u32x4*>(k_rd + kb + kt * 32 * KSTR + 64 * s);
+    const u32x4 hi = *reinterpret_cast<const u32x4*>(k_rd + kb + kt * 32 * KSTR + 64 * s + 16);
+    return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+  };
   auto qk_mma = [&](auto BUF) __attribute__((always_inline)) {
-    constexpr int kb = decltype(BUF)::value ? kK1 : kK0;
+    constexpr int kb = decltype(BUF)::value ? KB1 : 0;
+    if constexpr (kF8) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+          S[kt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(k_frag8(kb, kt, s), qf8[s], s == 0 ? zero16 : S[kt],
+                                                                 0, 0, 0, 0, 0, 0);
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < 8; ++s)
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(k_rd + kb + kt * 32 * kKStride + 32 * s);
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(k_rd + kb + kt * 32 * KSTR + 32 * s);
         S[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], s == 0 ? zero16 : S[kt], 0, 0, 0);
       }
   };
@@ -340,7 +384,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   // Nothing else touches LGKM in this phase (the barrier before it drained LDS and SMEM).
   auto mfma_phase = [&](auto PAR) __attribute__((always_inline)) {
     constexpr int par = decltype(PAR)::value;
-    constexpr int kb = (par ^ 1) ? kK1 : kK0;  // K(t+1)
+    constexpr int kb = (par ^ 1) ? KB1 : 0;  // K(t+1)
     constexpr int vb = par ? kVBuf : 0;         // V(t), relative to V0
     // lab only (tools/lab/build.sh -DCP25_LAB_QK_HALF / -DCP25_LAB_PV_HALF, wrong results): drop half of the
     // QK^T (k-steps 4-7) or P.V (k-steps 2-3) MFMAs and their operand reads, the MFMA and LDS work an fp8 operand
@@ -352,14 +396,14 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
 #define CP25_LAB_PV_HALF 0
 #endif
     constexpr auto lab_skip = [](int j) constexpr {
-      return (CP25_LAB_QK_HALF && j >= 8 && j < 16) || (CP25_LAB_PV_HALF && j >= 24 && j < 32);
+      return kF8 ? j < 16 : (CP25_LAB_QK_HALF && j >= 8 && j < 16) || (CP25_LAB_PV_HALF && j >= 24 && j < 32);
     };
     bf16x8 ring[5];
     auto issue = [&](auto JC) __attribute__((always_inline)) {
       constexpr int j = decltype(JC)::value;
       if constexpr (lab_skip(j)) {
       } else if constexpr (j < 16) {
-        constexpr int off = kb + (j & 1) * 32 * kKStride + 32 * (j >> 1);
+        constexpr int off = kb + (j & 1) * 32 * KSTR + 32 * (j >> 1);
         asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ring[j % 5]) : "v"(k_rd_lds), "i"(off));
       } else if constexpr (j < 32) {
         constexpr int off = vb + 16 * ((j - 16) >> 2) * kVStride + 64 * ((j - 16) & 3);
@@ -375,6 +419,16 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
     // the MFMA-phase wave outranks its softmax partner in issue arbitration (+8% measured)
     __builtin_amdgcn_s_setprio(1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the counted waits below assume an empty LGKM queue
+    if constexpr (kF8) {
+      // QK^T(t+1) on fp8: 4 MFMAs, their 8 reads compiler-scheduled, done before the P.V ring starts
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+          S[kt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(k_frag8(kb, kt, s), qf8[s], s == 0 ? zero16 : S[kt],
+                                                                 0, 0, 0, 0, 0, 0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     static_for<4>(issue);
     static_for<32>([&](auto JC) __attribute__((always_inline)) {
       constexpr int j = decltype(JC)::value;
@@ -1022,8 +1076,10 @@ extern "C" void cp25_attn_probe_set(unsigned long long* probe, int t0) { g_probe
 static int attn_launch(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq, int Lk, int D,
                        const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
                        const int64_t* o_strides, float softmax_scale, float q_norm_bound, float k_norm_bound,
-                       int n_split, void* workspace, size_t ws_bytes, hipStream_t stream, bool prescaled = false) {
+                       int n_split, void* workspace, size_t ws_bytes, hipStream_t stream, bool prescaled = false,
+                       bool fp8qk = false) {
   if (D != kD) return CP25_ERR_DTYPE;
+  if (fp8qk && !prescaled) return CP25_ERR_INVAL;
   if (prescaled && !(q_norm_bound > 0.f && k_norm_bound > 0.f && (double)q_norm_bound * k_norm_bound <= (double)kTop))
     return CP25_ERR_INVAL;
   if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0) return CP25_ERR_INVAL;
@@ -1035,9 +1091,9 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
   const int64_t* ss[4] = {q_strides, k_strides, v_strides, o_strides};
   for (int i = 0; i < 4; ++i)
     for (int j = 0; j < 3; ++j)
-      if (ss[i][j] % 8 != 0) return CP25_ERR_INVAL;
+      if (ss[i][j] % (fp8qk && i < 2 ? 16 : 8) != 0) return CP25_ERR_INVAL;  // 16 B in elements of the operand
   // buffer_load offsets within a 64-key tile are 32-bit
-  if ((int64_t)kKBlk * k_strides[1] * 2 >= (1ll << 31) || (int64_t)kKBlk * v_strides[1] * 2 >= (1ll << 31))
+  if ((int64_t)kKBlk * k_strides[1] * (fp8qk ? 1 : 2) >= (1ll << 31) || (int64_t)kKBlk * v_strides[1] * 2 >= (1ll << 31))
     return CP25_ERR_INVAL;
   if (k_strides[1] <= 0 || v_strides[1] <= 0) return CP25_ERR_INVAL;
   if (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) & 15) return CP25_ERR_INVAL;
@@ -1073,7 +1129,10 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
 #endif
   const int64_t nwg = (int64_t)a.nqb * B * H * n_split;
   if (nwg > 0x7fffffff) return CP25_ERR_INVAL;
-  if ((prescaled || fixed) && use_1w()) {
+  if (fp8qk) {
+    auto kernel = Lk <= 4096 ? attn_fwd_d128<1, true, true, true> : attn_fwd_d128<0, true, true, true>;
+    hipLaunchKernelGGL(kernel, dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
+  } else if ((prescaled || fixed) && use_1w()) {
     const bool dma = attn_variant() == 2;
     auto kernel = dma ? (prescaled ? (Lk <= 4096 ? attn_fwd_1w<1, true, true> : attn_fwd_1w<0, true, true>)
                                    : (Lk <= 4096 ? attn_fwd_1w<1, false, true> : attn_fwd_1w<0, false, true>))
@@ -1094,6 +1153,15 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
     CP25_LAUNCH_CHECK();
   }
   return CP25_OK;
+}
+
+extern "C" int cp25_attn_fwd_prescaled_fp8qk(const void* q8, const void* k8, const void* v, void* o, int B, int H,
+                                             int Lq, int Lk, int D, const int64_t* q_strides,
+                                             const int64_t* k_strides, const int64_t* v_strides,
+                                             const int64_t* o_strides, float q_norm_bound, float k_norm_bound,
+                                             int n_split, void* workspace, size_t ws_bytes, hipStream_t stream) {
+  return attn_launch(q8, k8, v, o, B, H, Lq, Lk, D, q_strides, k_strides, v_strides, o_strides, 0.6931471805599453f,
+                     q_norm_bound, k_norm_bound, n_split, workspace, ws_bytes, stream, true, true);
 }
 
 extern "C" size_t cp25_attn_workspace_bytes(int B, int H, int Lq, int n_split) {

@@ -134,7 +134,47 @@ int launch_quant(const void* x, void* q, float* s, int64_t n_rows, int64_t k, hi
   return CP25_OK;
 }
 
+// dst[r, c] = e4m3(bf16 src[r, c] * scale), saturated to +-448, round to nearest even: the fixed power-of-two
+// scaled fp8 copy of q and k for cp25_attn_fwd_prescaled_fp8qk. One thread per 16 elements (two 16-B loads,
+// one 16-B store); width % 16 == 0. HBM-bound.
+__global__ void __launch_bounds__(256) cast_fp8_kernel(const unsigned short* __restrict__ src, int64_t src_stride,
+                                                       unsigned char* __restrict__ dst, int64_t dst_stride,
+                                                       int64_t n_rows, int cpr, float scale) {
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= n_rows * cpr) return;
+  const int64_t r = gid / cpr;
+  const int c = (int)(gid % cpr) * 16;
+  const u32x4 a = *reinterpret_cast<const u32x4*>(src + r * src_stride + c);
+  const u32x4 b = *reinterpret_cast<const u32x4*>(src + r * src_stride + c + 8);
+  u32x4 o;
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    const unsigned w0 = h < 2 ? a[2 * h] : b[2 * h - 4], w1 = h < 2 ? a[2 * h + 1] : b[2 * h - 3];
+    float f[4] = {__uint_as_float(w0 << 16), __uint_as_float(w0 & 0xffff0000u), __uint_as_float(w1 << 16),
+                  __uint_as_float(w1 & 0xffff0000u)};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) f[e] = fminf(fmaxf(f[e] * scale, -kFp8Max), kFp8Max);
+    int w = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], w, true);
+    o[h] = (unsigned)w;
+  }
+  *reinterpret_cast<u32x4*>(dst + r * dst_stride + c) = o;
+}
+
 }  // namespace
+
+extern "C" int cp25_cast_fp8_e4m3(const void* src, int64_t src_stride, void* dst, int64_t dst_stride, int64_t n_rows,
+                                  int64_t width, float scale, hipStream_t stream) {
+  if (!src || !dst || n_rows <= 0 || width <= 0 || width % 16 || src_stride < width || dst_stride < width ||
+      (src_stride % 8) || (dst_stride % 16) || (((uintptr_t)src | (uintptr_t)dst) & 15) || !(scale > 0.f))
+    return CP25_ERR_INVAL;
+  const int cpr = (int)(width / 16);
+  const int64_t n = n_rows * cpr;
+  hipLaunchKernelGGL(cast_fp8_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, stream, (const unsigned short*)src,
+                     src_stride, (unsigned char*)dst, dst_stride, n_rows, cpr, scale);
+  CP25_LAUNCH_CHECK();
+  return CP25_OK;
+}
 
 extern "C" int cp25_quant_fp8_rows(const void* x, void* q, float* scale, int64_t n_rows, int64_t k,
                                    hipStream_t stream) {

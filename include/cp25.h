@@ -75,6 +75,22 @@ int cp25_attn_fwd_prescaled(const void* q, const void* k, const void* v, void* o
                             const int64_t* o_strides, float q_norm_bound, float k_norm_bound, int n_split,
                             void* workspace, size_t ws_bytes, hipStream_t stream);
 
+/* dst[r, c] = OCP e4m3(bf16 src[r, c] * scale) (saturated to +-448, round to nearest even), row strides in
+ * elements; width % 16 == 0. The fixed-scale fp8 copies of q and k for cp25_attn_fwd_prescaled_fp8qk. */
+int cp25_cast_fp8_e4m3(const void* src, int64_t src_stride, void* dst, int64_t dst_stride, int64_t n_rows,
+                       int64_t width, float scale, hipStream_t stream);
+
+/* The config-5 fp8 option's attention: cp25_attn_fwd_prescaled with q and k given as OCP e4m3 (one byte per
+ * element; strides in elements = bytes, multiples of 16): q8 = e4m3(q * softmax_scale * log2(e) * 2^s),
+ * k8 = e4m3(k * 2^-s) (cp25_cast_fp8_e4m3; the power-of-two scales cancel in q k^T, so no per-score multiply
+ * returns). Q K^T runs on v_mfma_f32_32x32x64_f8f6f4; P and V stay bf16, o is bf16. The bounds are those of
+ * the scaled bf16 rows, as for cp25_attn_fwd_prescaled. No reference counterpart (the reference has no fp8
+ * path); replaces the same attention call. */
+int cp25_attn_fwd_prescaled_fp8qk(const void* q8, const void* k8, const void* v, void* o, int B, int H, int Lq, int Lk,
+                                  int D, const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
+                                  const int64_t* o_strides, float q_norm_bound, float k_norm_bound, int n_split,
+                                  void* workspace, size_t ws_bytes, hipStream_t stream);
+
 /* Bytes of workspace cp25_attn_fwd_split / _bounded need (0 for n_split <= 1). */
 size_t cp25_attn_workspace_bytes(int B, int H, int Lq, int n_split);
 

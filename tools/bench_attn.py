@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--normed", action="store_true", help="RMS-normalised q/k rows without passing the bounds")
     ap.add_argument("--prescaled", action="store_true",
                     help="with --bounded: q carries scale*log2(e) (the DiT's default form, cp25_attn_fwd_prescaled)")
+    ap.add_argument("--fp8qk", action="store_true",
+                    help="with --prescaled: Q K^T on e4m3 copies of q*4 and k/4 (cp25_attn_fwd_prescaled_fp8qk)")
     ap.add_argument("--lib", default="", help="lab build of libcp25.so to load instead of the in-tree one")
     a = ap.parse_args()
     if a.lib:
@@ -63,6 +65,15 @@ def main():
         q.copy_((q.float() * c).to(torch.bfloat16))
         nb = (nb[0] * c, nb[1])
         pre = dict(prescaled=True)
+        if a.fp8qk:
+            if a.fused:
+                cols = [buf.view(a.L * a.B, 3 * D)[:, i * D:(i + 1) * D] for i in range(2)]
+                q8, k8 = (N.cast_fp8(cols[i], s).view(a.L, a.B, a.H, 128).transpose(0, 1)
+                          for i, s in ((0, 4.0), (1, 0.25)))
+            else:
+                q8 = N.cast_fp8(q.reshape(-1, 128), 4.0).view(q.shape)
+                k8 = N.cast_fp8(k.reshape(-1, 128), 0.25).view(k.shape)
+            pre["fp8_qk"] = (q8, k8)
     # correctness of the loaded build on a small shape (ragged length) vs fp32 math
     gc = torch.Generator(device=dev).manual_seed(1)
     qc, kc, vc = (torch.randn(1, 1000, 2, 128, device=dev, generator=gc).to(torch.bfloat16) for _ in range(3))
@@ -85,7 +96,7 @@ def main():
     ms = e0.elapsed_time(e1) / a.iters
     flop = 4.0 * a.B * a.H * a.L * Lk * 128
     print(json.dumps({"kernel": "attn_fwd", "B": a.B, "H": a.H, "Lq": a.L, "Lk": Lk, "fused": a.fused,
-                      "zeros": a.zeros, "bounded": a.bounded, "prescaled": a.prescaled, "normed": a.normed or a.bounded, "split": ns, "iters": a.iters, "lib": os.path.basename(a.lib) or "libcp25.so", "ms": ms,
+                      "zeros": a.zeros, "bounded": a.bounded, "prescaled": a.prescaled, "fp8qk": a.fp8qk, "normed": a.normed or a.bounded, "split": ns, "iters": a.iters, "lib": os.path.basename(a.lib) or "libcp25.so", "ms": ms,
                       "tflops": flop / ms / 1e9, "check_rel_l2": check}))
 
 
