@@ -26,12 +26,14 @@ def main():
     ap.add_argument("--num-steps", type=int, default=35)
     ap.add_argument("--chunk-size", type=int, default=12)
     ap.add_argument("--linear-precision", default="bf16", choices=("bf16", "fp8"))
+    ap.add_argument("--attention-precision", default="bf16", choices=("bf16", "fp8"))
     a = ap.parse_args()
     h, w = (int(x) for x in a.resolution.split(","))
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
     n_chunks = -(-(a.frames - 1) // a.chunk_size)
-    inf = ActionConditionedInference(device=dev, state_t=1 + a.chunk_size // 4, linear_precision=a.linear_precision)
+    inf = ActionConditionedInference(device=dev, state_t=1 + a.chunk_size // 4, linear_precision=a.linear_precision,
+                                     attention_precision=a.attention_precision)
     adim = inf.pipe.model.net.cfg.action_dim
     rng = np.random.RandomState(0)
     img = rng.randint(0, 256, size=(h, w, 3), dtype=np.uint8)
@@ -46,7 +48,8 @@ def main():
     assert video.shape == (a.frames, h, w, 3), video.shape
     print(json.dumps({"workload": f"action-conditioned AR {a.frames}f at {h}x{w}, {n_chunks} chunks of "
                                   f"{a.chunk_size + 1} frames, {a.num_steps} UniPC steps, CFG 7",
-                      "linear_precision": a.linear_precision, "n_gpus": 1, "seconds": dt,
+                      "linear_precision": a.linear_precision,
+                      "attention_precision": a.attention_precision, "n_gpus": 1, "seconds": dt,
                       "frames_per_s": a.frames / dt, "s_per_chunk": dt / n_chunks}), flush=True)
 
 
