@@ -90,6 +90,7 @@ struct AttnArgs {
   int nqb;          // query blocks per (b, h)
   int nsplit;       // key-range splits per (b, h, query block) (1: O written directly)
   int tps;          // key tiles per split
+  int nchunk;       // persistent short-KV form: workgroups per (b, h), each a contiguous run of query blocks
   float* o_part;    // nsplit > 1: [nsplit][B][H][Lq][128] fp32 partial O (normalised per split)
   float* lse_part;  // nsplit > 1: [nsplit][B][H][Lq] fp32 log2-sum-exp2 of the scaled scores
   float scale_log2; // softmax scale * log2(e)
@@ -131,10 +132,17 @@ struct AttnArgs {
 // bytes) and S^T = K Q^T runs on v_mfma_f32_32x32x64_f8f6f4: 4 MFMAs of 64 k per tile instead of 16 of 16,
 // K tiles of 64 rows x 128 B (LDS rows 144 B). P and V stay bf16. The operand k order only has to agree between
 // A and B: lane half h, byte i of both operands is d = 64 s + 32 h + i.
-template <int kKind, bool kFixed, bool kPre = false, bool kF8 = false>
+// kPersist (cross-attention, Lk <= 1024, cp25_attn_fwd_prescaled): one workgroup per CU runs a contiguous run of
+// query blocks of one (b, h) as one stream of key tiles (tile t = key tile t % ntk of block t / ntk). The
+// pipeline never drains between blocks: after the MFMA phase that closes a block, the wave stores that block's
+// O (and zeroes it) in its next VALU phase, and Q of the next block is reloaded right after the phase that ran
+// the old Q's last Q K^T. Without it, the 8 key tiles of a 512-key cross-attention paid the whole per-workgroup
+// prologue / epilogue (about 44 tiles of fixed cost, plan_split's fitted model) for every 256 queries.
+template <int kKind, bool kFixed, bool kPre = false, bool kF8 = false, bool kPersist = false>
 __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
   static_assert(!kF8 || kPre, "the fp8 Q K^T form is the prescaled one");
+  static_assert(!kPersist || (kPre && !kF8), "the persistent form is the prescaled bf16 one");
   constexpr int KSTR = kF8 ? 144 : kKStride;        // K LDS row stride
   constexpr int KB1 = kKBlk * KSTR;                 // K buffer 1
   constexpr int VB0 = 2 * kKBlk * KSTR, VB1 = VB0 + kVBuf;
@@ -143,8 +151,10 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   const int nwg = gridDim.x;
   const int tile = xcd_remap(blockIdx.x, nwg);
   // tile order (b, h) > split > query block: an XCD's contiguous tile range streams one key range
-  const int qb = tile % a.nqb, bhs = tile / a.nqb;
-  const int split = bhs % a.nsplit, bh = bhs / a.nsplit;
+  const int qb = kPersist ? (int)((int64_t)(tile % a.nchunk) * a.nqb / a.nchunk) : tile % a.nqb;
+  const int bhs = kPersist ? tile / a.nchunk : tile / a.nqb;
+  const int split = kPersist ? 0 : bhs % a.nsplit, bh = kPersist ? bhs : bhs / a.nsplit;
+  const int nblk = kPersist ? (int)((int64_t)(tile % a.nchunk + 1) * a.nqb / a.nchunk) - qb : 1;
   const int b = bh / a.H, h = bh % a.H;
   // this workgroup's keys: [split * tps * 64, ...) as a self-contained key sequence of length Lk
   const int key0 = split * a.tps * kKBlk;
@@ -204,7 +214,8 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
     m_run = fmaxf(sqrtf(qq) * a.kbound * a.scale_log2 - kTop, 0.f);
   }
 
-  const int ntiles = (Lk + kKBlk - 1) / kKBlk;
+  const int ntk = (Lk + kKBlk - 1) / kKBlk;       // key tiles per query block
+  const int ntiles = kPersist ? nblk * ntk : ntk;  // key tiles this workgroup streams
 
   // staging: a group's 256 threads own 4 chunks (16 B) each of a 64x128 tile: rows u/16 + 16 i,
   // chunk u%16. buffer_load: the tile base is a wave-uniform descriptor (SALU only), the per-lane
@@ -220,7 +231,8 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   const int st_off = (int)(srow * sl * esz) + sch * 16, st_step = (int)((kf8 ? 32 : 16) * sl * esz);
   const int nst = kf8 ? 2 : 4;
   u32x4 st[4];
-  auto load_tile = [&](int t) __attribute__((always_inline)) {
+  auto load_tile = [&](int tt) __attribute__((always_inline)) {
+    const int t = kPersist ? tt % ntk : tt;
     const int rows = min(Lk - t * kKBlk, kKBlk);
     const int nbytes = rows > 0 ? (int)((rows - 1) * sl * esz) + esz * kD : 0;
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(sbase + (int64_t)t * kKBlk * sl * esz), (short)0,
@@ -292,15 +304,18 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   };
   // online softmax of tile t: running max (O rescale skipped exactly when no row max of the wave
   // grew), P = exp2(S c - m) -> bf16 (lane-local B operand of P.V), row sum
-  auto softmax = [&](int t) __attribute__((always_inline)) {
+  auto softmax = [&](int tt) __attribute__((always_inline)) {
+    const int t = kPersist ? tt % ntk : tt;
     if (__builtin_expect(t == ragged_tile, 0)) {
+      // the keys left in this tile, opaque to the compiler: otherwise (t == ragged_tile is loop invariant) it
+      // hoists all 32 lane masks out of the tile loop, 64 SGPRs that the persistent form spills
+      int left = Lk - t * kKBlk - 4 * hl;
+      if constexpr (kPersist) asm volatile("" : "+v"(left));
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = t * kKBlk + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-          if (key >= Lk) S[kt][r] = -INFINITY;
-        }
+        for (int r = 0; r < 16; ++r)
+          if (kt * 32 + (r & 3) + 8 * (r >> 2) >= left) S[kt][r] = -INFINITY;
     }
     // S enters here: keeps the (otherwise dependency-free) bounded-shift exp work from being
     // hoisted across the barrier into the MFMA phase, where it would double the live P registers
@@ -360,6 +375,49 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   typedef std::integral_constant<int, 0> B0;
   typedef std::integral_constant<int, 1> B1;
 
+  // kPersist, after the MFMA phase of tile t (in the wave's next VALU phase): t closed its block -> store
+  // and zero O; t + 2 opens a block -> its Q, read by the next phase's Q K^T(t + 2)
+  // buffer descriptors (SGPRs) + one VGPR byte offset per access, the d offsets as immediates: plain pointers
+  // here had the compiler hoist 16 store and 8 load addresses out of the tile loop and spill (host-checked:
+  // Lq * row stride fits 31 bits)
+  const auto q_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)qp, (short)0, 0x7fffffff, 0x00020000);
+  const auto o_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(a.o + b * a.o_sb + h * a.o_sh), (short)0, 0x7fffffff, 0x00020000);
+  auto reload_q = [&](int t) __attribute__((always_inline)) {
+    if ((t + 2) % ntk == 0 && t + 2 < ntiles) {
+      const int row = min((qb + (t + 2) / ntk) * kQBlk + wave * kQRows + l31, a.Lq - 1);
+      const int off = row * (int)a.q_sl * 2 + 16 * hl;
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+        qf[s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(q_rsrc, off + 32 * s, 0, 0));
+    }
+  };
+  auto block_boundary = [&](int t) __attribute__((always_inline)) {
+    if ((t + 1) % ntk == 0) {
+      const int row = (qb + t / ntk) * kQBlk + wave * kQRows + l31;
+      const float inv = 1.f / wave_swap_sum(l_run);
+      if (row < a.Lq) {
+        const int off = row * (int)a.o_sl * 2 + 8 * hl;
+#pragma unroll
+        for (int db = 0; db < 4; ++db)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            u16x4 w;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) w[e] = f2bf(o[db][4 * g + e] * inv);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, w), o_rsrc, off + 2 * (32 * db + 8 * g), 0, 0);
+            __builtin_amdgcn_sched_barrier(0);  // one 4-value group at a time: no 64 live products
+          }
+      }
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+      l_run = 0.f;
+    }
+    reload_q(t);
+  };
+
   // ---- prologue: K(0), V(0) -> buffer 0; K(1) -> buffer 1; S(0) for everyone, P(0) for A ----
   load_tile(0);
   if (group_b) write_k(B0{}); else write_v(B0{});
@@ -372,6 +430,9 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   }
   __syncthreads();
   qk_mma(B0{});
+  if constexpr (kPersist) {
+    if (ntk == 1) reload_q(-1);  // one-tile blocks: Q of block 1 for Q K^T(1)
+  }
   if (!group_b) softmax(0);
   __syncthreads();
 
@@ -456,9 +517,12 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
         // the staged V(t+1) goes to LDS before the softmax: its LDS write drains under the VALU
         // (+0.9 % measured against writing after the softmax)
         write_v(std::integral_constant<int, par ^ 1>{});
+        if constexpr (kPersist) block_boundary(t);
         softmax(t + 1);
         ATTN_STAMP(t, 5);
         load_tile(t + 2);
+      } else if constexpr (kPersist) {
+        block_boundary(t);
       }
       ATTN_STAMP(t, 2);
       __syncthreads();
@@ -484,6 +548,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
       ATTN_STAMP(t, 2);
       __syncthreads();
       ATTN_STAMP(t, 3);
+      if constexpr (kPersist) block_boundary(t);
     };
     // pairs of tiles (constexpr buffer parity), then the odd last tile: one loop exit
     for (int t = 0; t + 1 < ntiles; t += 2) {
@@ -493,6 +558,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
     if (ntiles & 1) step(B0{}, ntiles - 1);
   }
 
+  if constexpr (kPersist) return;  // every block was stored at its boundary
   // ---- epilogue: O = O^T / l, bf16, row q, d = 32db + 8g + 4hl + (0..3) ----
   const float l_tot = wave_swap_sum(l_run);
   const float inv = 1.f / l_tot;
@@ -1031,6 +1097,14 @@ int attn_variant() {  // 0: 2w, 1: 1w, 2: 1w + DMA staging
 }
 bool use_1w() { return attn_variant() != 0; }
 
+// CP25_XATTN_KERNEL=persist: the persistent short-KV form (opt-in: measured 3 % slower than one workgroup per
+// query block at the DiT's cross-attention shape); read per launch (A/B runs and the
+// bit-exactness test switch it in-process)
+bool xattn_persistent() {
+  const char* e = getenv("CP25_XATTN_KERNEL");
+  return e && e[0] == 'p';
+}
+
 int num_cus() {
   if (g_num_cus == 0) {
     int dev = 0, n = 0;
@@ -1117,6 +1191,7 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
   a.nqb = (int)cdiv(Lq, kQBlk);
   a.nsplit = n_split;
   a.tps = (int)tps;
+  a.nchunk = 1;
   a.o_part = n_split > 1 ? (float*)workspace : nullptr;
   a.lse_part = n_split > 1 ? (float*)workspace + (size_t)n_split * rows * kD : nullptr;
   a.scale_log2 = softmax_scale * 1.4426950408889634f;
@@ -1139,6 +1214,14 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
                       : (prescaled ? (Lk <= 4096 ? attn_fwd_1w<1, true> : attn_fwd_1w<0, true>)
                                    : (Lk <= 4096 ? attn_fwd_1w<1, false> : attn_fwd_1w<0, false>));
     hipLaunchKernelGGL(kernel, dim3((unsigned)nwg), dim3(kThreads1w), 0, stream, a);
+  } else if (prescaled && Lk <= 1024 && n_split == 1 && xattn_persistent() &&
+             (int64_t)Lq * std::max(q_strides[1], o_strides[1]) * 2 < (1ll << 31)) {
+    // short-KV (text cross-attention): one workgroup per CU over a contiguous run of query blocks
+    const int64_t bhn = (int64_t)B * H;
+    a.nchunk = (int)std::min<int64_t>(std::max<int64_t>(num_cus() / bhn, 1), a.nqb);
+    if (bhn * a.nchunk > 0x7fffffff) return CP25_ERR_INVAL;
+    hipLaunchKernelGGL((attn_fwd_d128<1, true, true, false, true>), dim3((unsigned)(bhn * a.nchunk)), dim3(kThreads), 0,
+                       stream, a);
   } else {
     auto kernel = prescaled ? (Lk <= 4096 ? attn_fwd_d128<1, true, true> : attn_fwd_d128<0, true, true>)
                   : Lk <= 4096 ? (fixed ? attn_fwd_d128<1, true> : attn_fwd_d128<1, false>)
