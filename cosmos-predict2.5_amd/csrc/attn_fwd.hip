@@ -309,13 +309,23 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
     if (__builtin_expect(t == ragged_tile, 0)) {
       // the keys left in this tile, opaque to the compiler: otherwise (t == ragged_tile is loop invariant) it
       // hoists all 32 lane masks out of the tile loop, 64 SGPRs that the persistent form spills
-      int left = Lk - t * kKBlk - 4 * hl;
-      if constexpr (kPersist) asm volatile("" : "+v"(left));
+      if constexpr (kPersist) {
+        int left = Lk - t * kKBlk - 4 * hl;
+        asm volatile("" : "+v"(left));
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+        for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (kt * 32 + (r & 3) + 8 * (r >> 2) >= left) S[kt][r] = -INFINITY;
+          for (int r = 0; r < 16; ++r)
+            if (kt * 32 + (r & 3) + 8 * (r >> 2) >= left) S[kt][r] = -INFINITY;
+      } else {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = t * kKBlk + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+            if (key >= Lk) S[kt][r] = -INFINITY;
+          }
+      }
     }
     // S enters here: keeps the (otherwise dependency-free) bounded-shift exp work from being
     // hoisted across the barrier into the MFMA phase, where it would double the live P registers
