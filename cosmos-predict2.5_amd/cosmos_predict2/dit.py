@@ -209,6 +209,8 @@ class MinimalV1LVGDiT:
         self.exact_q_rounding = False
         # "bf16" (default) or "fp8": self-attention Q K^T on e4m3 copies of q and k (set_attention_precision)
         self.attention_precision = "bf16"
+        # the CFG pair's shared block-0 prefix runs once (see _blocks); False: every entry computes it
+        self.share_cfg_block0 = True
 
     def set_linear_precision(self, precision: str) -> None:
         """"bf16" (default, the reference's arithmetic) or "fp8": the 28 blocks' q/k/v, output, cross-q,
@@ -494,10 +496,11 @@ class MinimalV1LVGDiT:
 
     def forward_tokens(self, patch_rows: torch.Tensor, t_B_T: torch.Tensor, ctx: ContextCache,
                        geo: Geometry, action: Optional[torch.Tensor] = None,
-                       view_indices: Optional[torch.Tensor] = None) -> torch.Tensor:
+                       view_indices: Optional[torch.Tensor] = None, shared_batch: bool = False) -> torch.Tensor:
         """patch_rows: [n_tok, Bx, 72] bf16 (Bx = 1 shares the input across the CFG batch);
         t_B_T: [B, T] fp32, already scaled. Returns the final layer output [n_tok, B, 64] fp32
-        (feature order (p1 p2 C) = patch layout).
+        (feature order (p1 p2 C) = patch layout). shared_batch: the caller guarantees every batch entry
+        has the same t (and action), so with Bx = 1 they differ only in the text context (_blocks).
 
         CP = 1: one pass over the batch (B = 2 = [cond, uncond]).
         CP > 1: the batch entries run as two software-pipelined lanes on the current stream: each
@@ -518,7 +521,7 @@ class MinimalV1LVGDiT:
         cp = self.cp_group
         cp_size = 1 if cp is None else torch.distributed.get_world_size(cp)
         if B == 1 or (cp_size == 1 and not self.force_lanes):
-            gen = self._blocks(x_in, mods, shift_f, scale_f, ctx, geo, cos, sin, cp, cp_size)
+            gen = self._blocks(x_in, mods, shift_f, scale_f, ctx, geo, cos, sin, cp, cp_size, shared_batch)
             while True:
                 try:
                     next(gen)
@@ -532,51 +535,62 @@ class MinimalV1LVGDiT:
                                       sin, cp, cp_size))
         return torch.cat(run_lanes(lanes), dim=1)
 
-    def _blocks(self, x_in, mods, shift_f, scale_f, ctx: ContextCache, geo: Geometry, cos, sin, cp, cp_size):
+    def _blocks(self, x_in, mods, shift_f, scale_f, ctx: ContextCache, geo: Geometry, cos, sin, cp, cp_size,
+                shared_batch: bool = False):
         """Generator: issues the 28 blocks + final layer for the batch entries in x_in/mods/ctx on the
         current stream; returns the final layer output [n, B, 64] fp32. Yields (so the caller can
         issue the other lane) right after each self-attention K/V gather is queued (CP > 1), or after
-        each block (CP = 1)."""
+        each block (CP = 1).
+
+        shared_batch (the CFG pair: one input x, one t, one action, only the text context differs): block
+        0's self-attention sub-layer and its residual, and the cross-attention query, see identical
+        inputs in every batch entry, so they run once (B = 1) and the cross-attention reads that query
+        with batch stride 0 against each entry's own text K/V. Every later sub-layer has per-entry
+        inputs. Same values as running both entries (tests/test_dit_gpu.py::test_shared_cfg_block0)."""
         cfg = self.cfg
         p = self.sd
         B = ctx.B
         D, H, hd = cfg.model_channels, cfg.num_heads, cfg.head_dim
         n = geo.n_tok
         Bx = x_in.shape[1]
+        share0 = shared_batch and Bx == 1 and B > 1 and (cp is None or cp_size == 1) and self.share_cfg_block0
 
-        def mod(i, j):  # (shift, scale, gate) bf16 [B, T, D] views of block i, sub-layer j
-            m = mods[i, j]
+        def mod(i, j, nb=None):  # (shift, scale, gate) bf16 [B, T, D] views of block i, sub-layer j (first nb)
+            m = mods[i, j] if nb is None else mods[i, j][:nb]
             return m[..., :D], m[..., D:2 * D], m[..., 2 * D:]
 
         # fp8: each LN-mod emits its h straight as the next GEMM's fp8 operand (q, scale)
         common = dict(n_tok=n, B=B, tok0=geo.tok0, hw=geo.hw)
         lnk = dict(common, fp8=self.linear_precision == "fp8")
-        sh, sc, _ = mod(0, 0)
+        lnk1 = dict(lnk, B=1)
+        sh, sc, _ = mod(0, 0, 1 if share0 else None)
         x = x_in
-        h = N.ln_mod(x, sh, sc, x_st=x_in.stride(0), x_sb=0 if Bx == 1 else x_in.stride(1), **lnk)
+        h = N.ln_mod(x, sh, sc, x_st=x_in.stride(0), x_sb=0 if Bx == 1 else x_in.stride(1),
+                     **(lnk1 if share0 else lnk))
         y = None
         gate_prev = None
         for i in range(cfg.num_blocks):
             pre = f"blocks.{i}."
+            Bs = 1 if (share0 and i == 0) else B  # batch rows up to the cross-attention query
             # ---- self attention
-            o = torch.empty((n, B, D), dtype=BF16, device=self.device)
+            o = torch.empty((n, Bs, D), dtype=BF16, device=self.device)
             ev = None
             if self.attn_events is not None:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             if cp is None or cp_size == 1:
-                qkv = self._linear(_rows(h, n * B), self.w_qkv[i], f"qkv.{i}")  # [n*B, 3D]
+                qkv = self._linear(_rows(h, n * Bs), self.w_qkv[i], f"qkv.{i}")  # [n*Bs, 3D]
                 q_scale, attn_kw = self._self_attn_mode(i, hd)
-                N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=0,
+                N.head_rmsnorm_rope(qkv, n_rows=n * Bs, B=Bs, H=H, head_off=0,
                                     weight=p[pre + "self_attn.q_norm.weight"], cos=cos, sin=sin, out_scale=q_scale)
-                N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=D,
+                N.head_rmsnorm_rope(qkv, n_rows=n * Bs, B=Bs, H=H, head_off=D,
                                     weight=p[pre + "self_attn.k_norm.weight"], cos=cos, sin=sin)
-                q = qkv.view(n, B, 3 * D)[:, :, :D].view(n, B, H, hd).transpose(0, 1)
-                kk = qkv.view(n, B, 3 * D)[:, :, D:2 * D].view(n, B, H, hd).transpose(0, 1)
-                vv = qkv.view(n, B, 3 * D)[:, :, 2 * D:].view(n, B, H, hd).transpose(0, 1)
-                attn_kw = self._fp8_qk(qkv[:, :D], qkv[:, D:2 * D], B, H, hd, attn_kw)
+                q = qkv.view(n, Bs, 3 * D)[:, :, :D].view(n, Bs, H, hd).transpose(0, 1)
+                kk = qkv.view(n, Bs, 3 * D)[:, :, D:2 * D].view(n, Bs, H, hd).transpose(0, 1)
+                vv = qkv.view(n, Bs, 3 * D)[:, :, 2 * D:].view(n, Bs, H, hd).transpose(0, 1)
+                attn_kw = self._fp8_qk(qkv[:, :D], qkv[:, D:2 * D], Bs, H, hd, attn_kw)
                 if ev is not None:
                     ev[0].record()
-                N.attn_fwd(q, kk, vv, out=o.view(n, B, H, hd).transpose(0, 1), **attn_kw)
+                N.attn_fwd(q, kk, vv, out=o.view(n, Bs, H, hd).transpose(0, 1), **attn_kw)
                 lk = kk.shape[1]
             else:
                 yield from self._cp_self_attention(i, h, o, cos, sin, n, B, cp, cp_size,
@@ -584,30 +598,32 @@ class MinimalV1LVGDiT:
                 lk = cp_size * n
             if ev is not None:
                 ev[1].record()
-                self.attn_events.append((ev[0], ev[1], 4.0 * B * H * n * lk * hd))
-            y = self._linear(o.view(n * B, D), p[pre + "self_attn.output_proj.weight"], pre + "self_attn.output_proj")
+                self.attn_events.append((ev[0], ev[1], 4.0 * Bs * H * n * lk * hd))
+            y = self._linear(o.view(n * Bs, D), p[pre + "self_attn.output_proj.weight"], pre + "self_attn.output_proj")
             # ---- x += g_sa * y ; LN-mod for cross attention
-            _, _, g_sa = mod(i, 0)
-            sh, sc, _ = mod(i, 1)
-            x_new = torch.empty((n, B, D), dtype=BF16, device=self.device)
+            nb = 1 if Bs == 1 and B > 1 else None
+            _, _, g_sa = mod(i, 0, nb)
+            sh, sc, _ = mod(i, 1, nb)
+            x_new = torch.empty((n, Bs, D), dtype=BF16, device=self.device)
             if i == 0:
                 x_st, x_sb = x_in.stride(0), (0 if Bx == 1 else x_in.stride(1))
             else:
                 x_st, x_sb = B * D, D
-            h = N.ln_mod(x, sh, sc, x_st=x_st, x_sb=x_sb, y=y, gate=g_sa, x_out=x_new, **lnk)
+            h = N.ln_mod(x, sh, sc, x_st=x_st, x_sb=x_sb, y=y, gate=g_sa, x_out=x_new, **dict(lnk, B=Bs))
             x = x_new
-            # ---- cross attention
-            qc = self._linear(_rows(h, n * B), p[pre + "cross_attn.q_proj.weight"], pre + "cross_attn.q_proj")
+            # ---- cross attention (a shared query is read with batch stride 0 against each entry's text K/V)
+            qc = self._linear(_rows(h, n * Bs), p[pre + "cross_attn.q_proj.weight"], pre + "cross_attn.q_proj")
             xq_scale, xattn_kw = self._attn_mode(self.xattn_bounds[i], hd)  # prescaled q as in self-attention
-            N.head_rmsnorm_rope(qc, n_rows=n * B, B=B, H=H, head_off=0, weight=p[pre + "cross_attn.q_norm.weight"],
+            N.head_rmsnorm_rope(qc, n_rows=n * Bs, B=Bs, H=H, head_off=0, weight=p[pre + "cross_attn.q_norm.weight"],
                                 out_scale=xq_scale)
             o = torch.empty((n, B, D), dtype=BF16, device=self.device)
-            self._cross_attention(qc.view(n, B, H, hd), ctx.k[i], ctx.v[i], o.view(n, B, H, hd), geo, xattn_kw)
+            self._cross_attention(qc.view(n, Bs, H, hd).expand(n, B, H, hd), ctx.k[i], ctx.v[i], o.view(n, B, H, hd),
+                                  geo, xattn_kw)
             y = self._linear(o.view(n * B, D), p[pre + "cross_attn.output_proj.weight"], pre + "cross_attn.output_proj")
             _, _, g_ca = mod(i, 1)
             sh, sc, _ = mod(i, 2)
             x_new = torch.empty((n, B, D), dtype=BF16, device=self.device)
-            h = N.ln_mod(x, sh, sc, x_st=B * D, x_sb=D, y=y, gate=g_ca, x_out=x_new, **lnk)
+            h = N.ln_mod(x, sh, sc, x_st=Bs * D, x_sb=0 if Bs == 1 else D, y=y, gate=g_ca, x_out=x_new, **lnk)
             x = x_new
             # ---- MLP
             u = self._linear(_rows(h, n * B), p[pre + "mlp.layer1.weight"], pre + "mlp.layer1")

@@ -282,8 +282,10 @@ class SamplingRun:
         tf = m._frame_timesteps(t, self.frame_mask)  # [T]
         t_B_T = (tf[None, :] * m.net_cfg.timestep_scale).expand(2, geo.T).contiguous()
         if self.net_fn is None:
+            # one t row expanded over the CFG pair, one action: the entries differ only in the text context
+            shared = self.action is None or self.action.shape[0] == 1
             net_out = m.net.forward_tokens(rows.view(geo.n_tok, 1, -1), t_B_T, self.ctx, geo, action=self.action,
-                                           view_indices=self.view_indices)
+                                           view_indices=self.view_indices, shared_batch=shared)
         else:
             net_out = self.net_fn(rows.view(geo.n_tok, 1, -1), t_B_T, geo)
         v = N.cfg_velocity(net_out, self.noise, self.gtp, self.frame_mask, self.guidance, self.mode,

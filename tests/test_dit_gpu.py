@@ -224,3 +224,43 @@ def test_config1_shape_2b_width_sampler_matches_oracle(device):
     err = rel_l2(out.cpu(), ref)
     print(f"config-1 shape, 2B widths (2 blocks) sampler vs oracle rel-L2: {err:.3e}")
     assert err <= 1e-2, err
+
+
+@pytest.mark.parametrize("two_b", [False, True])
+def test_shared_cfg_block0(device, two_b):
+    """The CFG pair shares x, t and the action, so block 0's self-attention sub-layer, its residual and the
+    cross-attention query run once (MinimalV1LVGDiT._blocks, shared_batch). Tiny widths: the same trajectory
+    bit for bit as with every entry computing them (share_cfg_block0 = False). 2B widths: the library GEMMs
+    pick other kernels for n rows than for 2n (accumulation order, bf16 rounding of some outputs), so the
+    check is against the oracle: the shared path is as close to it as the per-entry path (guidance 0, where
+    the CFG difference is not amplified)."""
+    from cosmos_predict2.net_config import DIT_2B
+
+    cfg = DIT_2B.replace(num_blocks=2) if two_b else tiny_dit(num_blocks=2)
+    _, sd_ref = _setup(cfg, seed=5)
+    T, H, W = (3, 32, 32) if two_b else (3, 16, 16)
+    g = torch.Generator().manual_seed(50)
+    gt = torch.randn(1, 16, T, H, W, generator=g)
+    ctx_c = torch.randn(1, 512, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
+    ctx_u = torch.randn(1, 512, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
+    model = Video2WorldModelRectifiedFlow(cfg, SamplerConfig(use_kerras_sigma_at_inference=True,
+                                                             conditional_frame_timestep=0.1), device=device)
+    model.load_state_dict(sd_ref)
+    guidance = 0.0 if two_b else 7.0
+    outs = []
+    for share in (True, False):
+        model.net.share_cfg_block0 = share
+        outs.append(model.sample_latents(gt.to(device), ctx_c.to(device), ctx_u.to(device),
+                                         state_shape=(16, T, H, W), num_conditional_frames=1, guidance=guidance,
+                                         seed=0, num_steps=2).cpu())
+    model.net.share_cfg_block0 = True
+    assert torch.isfinite(outs[0]).all()
+    if not two_b:
+        assert torch.equal(outs[0], outs[1])
+        return
+    ref = osamp.generate(dataclasses.asdict(cfg), sd_ref, gt, ctx_c, ctx_u, num_cond=1, guidance=guidance, seed=0,
+                         num_steps=2, use_karras=True, cond_frame_t=0.1)
+    e_sh, e_pe = rel_l2(outs[0], ref), rel_l2(outs[1], ref)
+    print(f"shared block-0 prefix (2B widths, g=0): vs oracle {e_sh:.3e}, per-entry path {e_pe:.3e}, "
+          f"shared vs per-entry {rel_l2(outs[0], outs[1]):.3e}")
+    assert e_sh <= 1e-2 and e_sh <= 1.2 * e_pe, (e_sh, e_pe)
