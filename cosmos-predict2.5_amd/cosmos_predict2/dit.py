@@ -528,15 +528,26 @@ class MinimalV1LVGDiT:
                 except StopIteration as e:
                     return e.value
         lanes = []
+        prefix = None
+        if shared_batch and Bx == 1 and self.share_cfg_block0:
+            # the entries' identical block-0 prefix once (its K/V gather waited on in place), then the lanes
+            cb = ContextCache(B=1, k=[t[:1] for t in ctx.k], v=[t[:1] for t in ctx.v])
+            gen = self._blocks(x_in, mods[:, :, :1], shift_f[:1], scale_f[:1], cb, geo, cos, sin, cp, cp_size,
+                               prefix_only=True)
+            while prefix is None:
+                try:
+                    next(gen)
+                except StopIteration as e:
+                    prefix = e.value
         for b in range(B):
             cb = ContextCache(B=1, k=[t[b:b + 1] for t in ctx.k], v=[t[b:b + 1] for t in ctx.v])
             xb = x_in[:, (0 if Bx == 1 else b):(0 if Bx == 1 else b) + 1]
             lanes.append(self._blocks(xb, mods[:, :, b:b + 1], shift_f[b:b + 1], scale_f[b:b + 1], cb, geo, cos,
-                                      sin, cp, cp_size))
+                                      sin, cp, cp_size, prefix=prefix))
         return torch.cat(run_lanes(lanes), dim=1)
 
     def _blocks(self, x_in, mods, shift_f, scale_f, ctx: ContextCache, geo: Geometry, cos, sin, cp, cp_size,
-                shared_batch: bool = False):
+                shared_batch: bool = False, prefix=None, prefix_only: bool = False):
         """Generator: issues the 28 blocks + final layer for the batch entries in x_in/mods/ctx on the
         current stream; returns the final layer output [n, B, 64] fp32. Yields (so the caller can
         issue the other lane) right after each self-attention K/V gather is queued (CP > 1), or after
@@ -546,7 +557,9 @@ class MinimalV1LVGDiT:
         0's self-attention sub-layer and its residual, and the cross-attention query, see identical
         inputs in every batch entry, so they run once (B = 1) and the cross-attention reads that query
         with batch stride 0 against each entry's own text K/V. Every later sub-layer has per-entry
-        inputs. Same values as running both entries (tests/test_dit_gpu.py::test_shared_cfg_block0)."""
+        inputs. Same values as running both entries (tests/test_dit_gpu.py::test_shared_cfg_block0).
+        CP lanes (one entry each) share it the same way: prefix_only=True runs block 0 up to the cross-attention
+        LN-mod for one entry and returns (x, h); each lane then starts from prefix=(x, h)."""
         cfg = self.cfg
         p = self.sd
         B = ctx.B
@@ -563,54 +576,62 @@ class MinimalV1LVGDiT:
         common = dict(n_tok=n, B=B, tok0=geo.tok0, hw=geo.hw)
         lnk = dict(common, fp8=self.linear_precision == "fp8")
         lnk1 = dict(lnk, B=1)
-        sh, sc, _ = mod(0, 0, 1 if share0 else None)
-        x = x_in
-        h = N.ln_mod(x, sh, sc, x_st=x_in.stride(0), x_sb=0 if Bx == 1 else x_in.stride(1),
-                     **(lnk1 if share0 else lnk))
+        if prefix is None:
+            sh, sc, _ = mod(0, 0, 1 if share0 else None)
+            x = x_in
+            h = N.ln_mod(x, sh, sc, x_st=x_in.stride(0), x_sb=0 if Bx == 1 else x_in.stride(1),
+                         **(lnk1 if share0 else lnk))
+        else:
+            x, h = prefix
         y = None
         gate_prev = None
         for i in range(cfg.num_blocks):
             pre = f"blocks.{i}."
             Bs = 1 if (share0 and i == 0) else B  # batch rows up to the cross-attention query
-            # ---- self attention
-            o = torch.empty((n, Bs, D), dtype=BF16, device=self.device)
-            ev = None
-            if self.attn_events is not None:
-                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            if cp is None or cp_size == 1:
-                qkv = self._linear(_rows(h, n * Bs), self.w_qkv[i], f"qkv.{i}")  # [n*Bs, 3D]
-                q_scale, attn_kw = self._self_attn_mode(i, hd)
-                N.head_rmsnorm_rope(qkv, n_rows=n * Bs, B=Bs, H=H, head_off=0,
-                                    weight=p[pre + "self_attn.q_norm.weight"], cos=cos, sin=sin, out_scale=q_scale)
-                N.head_rmsnorm_rope(qkv, n_rows=n * Bs, B=Bs, H=H, head_off=D,
-                                    weight=p[pre + "self_attn.k_norm.weight"], cos=cos, sin=sin)
-                q = qkv.view(n, Bs, 3 * D)[:, :, :D].view(n, Bs, H, hd).transpose(0, 1)
-                kk = qkv.view(n, Bs, 3 * D)[:, :, D:2 * D].view(n, Bs, H, hd).transpose(0, 1)
-                vv = qkv.view(n, Bs, 3 * D)[:, :, 2 * D:].view(n, Bs, H, hd).transpose(0, 1)
-                attn_kw = self._fp8_qk(qkv[:, :D], qkv[:, D:2 * D], Bs, H, hd, attn_kw)
+            if prefix is not None and i == 0:
+                pass  # block 0 up to here ran once for every lane (prefix)
+            else:
+                # ---- self attention
+                o = torch.empty((n, Bs, D), dtype=BF16, device=self.device)
+                ev = None
+                if self.attn_events is not None:
+                    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                if cp is None or cp_size == 1:
+                    qkv = self._linear(_rows(h, n * Bs), self.w_qkv[i], f"qkv.{i}")  # [n*Bs, 3D]
+                    q_scale, attn_kw = self._self_attn_mode(i, hd)
+                    N.head_rmsnorm_rope(qkv, n_rows=n * Bs, B=Bs, H=H, head_off=0,
+                                        weight=p[pre + "self_attn.q_norm.weight"], cos=cos, sin=sin, out_scale=q_scale)
+                    N.head_rmsnorm_rope(qkv, n_rows=n * Bs, B=Bs, H=H, head_off=D,
+                                        weight=p[pre + "self_attn.k_norm.weight"], cos=cos, sin=sin)
+                    q = qkv.view(n, Bs, 3 * D)[:, :, :D].view(n, Bs, H, hd).transpose(0, 1)
+                    kk = qkv.view(n, Bs, 3 * D)[:, :, D:2 * D].view(n, Bs, H, hd).transpose(0, 1)
+                    vv = qkv.view(n, Bs, 3 * D)[:, :, 2 * D:].view(n, Bs, H, hd).transpose(0, 1)
+                    attn_kw = self._fp8_qk(qkv[:, :D], qkv[:, D:2 * D], Bs, H, hd, attn_kw)
+                    if ev is not None:
+                        ev[0].record()
+                    N.attn_fwd(q, kk, vv, out=o.view(n, Bs, H, hd).transpose(0, 1), **attn_kw)
+                    lk = kk.shape[1]
+                else:
+                    yield from self._cp_self_attention(i, h, o, cos, sin, n, B, cp, cp_size,
+                                                       ev[0] if ev is not None else None)
+                    lk = cp_size * n
                 if ev is not None:
-                    ev[0].record()
-                N.attn_fwd(q, kk, vv, out=o.view(n, Bs, H, hd).transpose(0, 1), **attn_kw)
-                lk = kk.shape[1]
-            else:
-                yield from self._cp_self_attention(i, h, o, cos, sin, n, B, cp, cp_size,
-                                                   ev[0] if ev is not None else None)
-                lk = cp_size * n
-            if ev is not None:
-                ev[1].record()
-                self.attn_events.append((ev[0], ev[1], 4.0 * Bs * H * n * lk * hd))
-            y = self._linear(o.view(n * Bs, D), p[pre + "self_attn.output_proj.weight"], pre + "self_attn.output_proj")
-            # ---- x += g_sa * y ; LN-mod for cross attention
-            nb = 1 if Bs == 1 and B > 1 else None
-            _, _, g_sa = mod(i, 0, nb)
-            sh, sc, _ = mod(i, 1, nb)
-            x_new = torch.empty((n, Bs, D), dtype=BF16, device=self.device)
-            if i == 0:
-                x_st, x_sb = x_in.stride(0), (0 if Bx == 1 else x_in.stride(1))
-            else:
-                x_st, x_sb = B * D, D
-            h = N.ln_mod(x, sh, sc, x_st=x_st, x_sb=x_sb, y=y, gate=g_sa, x_out=x_new, **dict(lnk, B=Bs))
-            x = x_new
+                    ev[1].record()
+                    self.attn_events.append((ev[0], ev[1], 4.0 * Bs * H * n * lk * hd))
+                y = self._linear(o.view(n * Bs, D), p[pre + "self_attn.output_proj.weight"], pre + "self_attn.output_proj")
+                # ---- x += g_sa * y ; LN-mod for cross attention
+                nb = 1 if Bs == 1 and B > 1 else None
+                _, _, g_sa = mod(i, 0, nb)
+                sh, sc, _ = mod(i, 1, nb)
+                x_new = torch.empty((n, Bs, D), dtype=BF16, device=self.device)
+                if i == 0:
+                    x_st, x_sb = x_in.stride(0), (0 if Bx == 1 else x_in.stride(1))
+                else:
+                    x_st, x_sb = B * D, D
+                h = N.ln_mod(x, sh, sc, x_st=x_st, x_sb=x_sb, y=y, gate=g_sa, x_out=x_new, **dict(lnk, B=Bs))
+                x = x_new
+            if prefix_only:
+                return x, h
             # ---- cross attention (a shared query is read with batch stride 0 against each entry's text K/V)
             qc = self._linear(_rows(h, n * Bs), p[pre + "cross_attn.q_proj.weight"], pre + "cross_attn.q_proj")
             xq_scale, xattn_kw = self._attn_mode(self.xattn_bounds[i], hd)  # prescaled q as in self-attention
