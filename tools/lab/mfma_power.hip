@@ -1,0 +1,85 @@
+// Lab: does MFMA throughput under sustained load depend on operand bit activity between consecutive MFMAs?
+// 256 CUs x 8 waves run back-to-back v_mfma_f32_32x32x16_bf16 on register operands with random bf16 data.
+//   pattern 0: A and B change every MFMA (8 distinct each)
+//   pattern 1: A changes every MFMA, B every 8
+//   pattern 2: A every 8, B every MFMA
+//   pattern 3: A and B never change
+//   pattern 4: pattern 0 on zero data
+// Prints TFLOP/s per pattern (hipEvent timing). Build: hipcc --offload-arch=gfx950 -O3 -o mfma_power mfma_power.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int P>
+__global__ void __launch_bounds__(512, 2) mfma_loop(const bf16x8* __restrict__ src, float* __restrict__ out, int iters) {
+  const int lane = threadIdx.x & 63;
+  bf16x8 a[8], b[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    a[i] = src[(i * 64 + lane) % 1024];
+    b[i] = src[((i + 8) * 64 + lane) % 1024];
+  }
+  f32x16 acc[4] = {};
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+      const int ia = (P == 0 || P == 1 || P == 4) ? (j & 7) : (P == 2 ? (j >> 3) & 7 : 0);
+      const int ib = (P == 0 || P == 2 || P == 4) ? (j & 7) : (P == 1 ? (j >> 3) & 7 : 0);
+      acc[j & 3] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ia], b[ib], acc[j & 3], 0, 0, 0);
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s += acc[c][r];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+template <int P>
+double run(const bf16x8* src, float* out, int iters) {
+  const int grid = 256 * 2, block = 512;
+  hipLaunchKernelGGL(mfma_loop<P>, dim3(grid), dim3(block), 0, 0, src, out, 10);
+  hipDeviceSynchronize();
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  hipEventRecord(e0);
+  hipLaunchKernelGGL(mfma_loop<P>, dim3(grid), dim3(block), 0, 0, src, out, iters);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, e0, e1);
+  const double flop = 2.0 * 32 * 32 * 16 * 64.0 * iters * (grid * block / 64);
+  return flop / (ms * 1e-3) / 1e12;
+}
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? atoi(argv[1]) : 20000;
+  std::vector<unsigned short> h(1024 * 8);
+  unsigned x = 12345u;
+  for (auto& v : h) {  // random bf16 of moderate magnitude: sign, exponent 120..133, random mantissa
+    x = x * 1664525u + 1013904223u;
+    v = (unsigned short)(((x >> 31) << 15) | (((x >> 20) % 14 + 120) << 7) | ((x >> 8) & 127));
+  }
+  bf16x8 *src, *zsrc;
+  float* out;
+  hipMalloc(&src, h.size() * 2);
+  hipMalloc(&zsrc, h.size() * 2);
+  hipMalloc(&out, 256 * 2 * 512 * 4);
+  hipMemcpy(src, h.data(), h.size() * 2, hipMemcpyHostToDevice);
+  hipMemset(zsrc, 0, h.size() * 2);
+  for (int rep = 0; rep < 2; ++rep) {
+    printf("pattern 0 (A, B change every MFMA): %.1f TFLOP/s\n", run<0>(src, out, iters));
+    printf("pattern 1 (A every MFMA, B every 8): %.1f TFLOP/s\n", run<1>(src, out, iters));
+    printf("pattern 2 (A every 8, B every MFMA): %.1f TFLOP/s\n", run<2>(src, out, iters));
+    printf("pattern 3 (A, B fixed): %.1f TFLOP/s\n", run<3>(src, out, iters));
+    printf("pattern 4 (pattern 0, zero data): %.1f TFLOP/s\n", run<4>(zsrc, out, iters));
+    fflush(stdout);
+  }
+  return 0;
+}
