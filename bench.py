@@ -52,8 +52,9 @@ def parse():
     ap.add_argument("--resolution", default="704,1280")
     ap.add_argument("--linear-precision", default="bf16", choices=("bf16", "fp8"),
                     help="fp8: the DiT block projections/MLP as fp8 MFMA GEMMs (config 5's option; not the metric)")
-    ap.add_argument("--attention-precision", default="bf16", choices=("bf16", "fp8"),
-                    help="fp8: self-attention Q K^T on e4m3 operands (config 5's option; not the metric)")
+    ap.add_argument("--attention-precision", default="bf16", choices=("bf16", "fp8qk", "fp8"),
+                    help="fp8qk: self-attention Q K^T on e4m3 operands; fp8: also P.V on e5m2 P / e4m3 V (config 5's "
+                         "option; not the metric)")
     ap.add_argument("--no-cfg-share", action="store_true",
                     help="every CFG entry computes block 0's shared self-attention prefix (A/B of the sharing)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -215,7 +216,8 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16" if (a.linear_precision, a.attention_precision) == ("bf16", "bf16") else
                      " + ".join(x for x, on in (("fp8 (block GEMMs)", a.linear_precision == "fp8"),
-                                                ("fp8 (attention Q K^T)", a.attention_precision == "fp8")) if on)
+                                                ("fp8 (attention Q K^T)", a.attention_precision == "fp8qk"),
+                                                ("fp8 (attention Q K^T, P.V)", a.attention_precision == "fp8")) if on)
                      + " + bf16",
             "data": "synthetic: seeded random 2B/VAE weights, random conditioning image, N(0,1) text embeddings",
             "config": {
@@ -239,8 +241,10 @@ def main():
             },
             "roofline": {
                 "bound": "mfma",
-                "kernel": "cp25_attn_fwd (DiT self-attention, bf16 MFMA)" if a.attention_precision == "bf16" else
-                          "cp25_attn_fwd_prescaled_fp8qk (DiT self-attention, fp8 Q K^T + bf16 P V MFMA)",
+                "kernel": {"bf16": "cp25_attn_fwd (DiT self-attention, bf16 MFMA)",
+                           "fp8qk": "cp25_attn_fwd_prescaled_fp8qk (DiT self-attention, fp8 Q K^T + bf16 P V MFMA)",
+                           "fp8": "cp25_attn_fwd_prescaled_fp8 (DiT self-attention, fp8 Q K^T and P V MFMA)"}[
+                               a.attention_precision],
                 "achieved": achieved,
                 "peak": BF16_DENSE_PEAK_TFLOPS,
                 "unit": "TFLOP/s",

@@ -58,6 +58,10 @@ SIGNATURES = {
     "cp25_attn_fwd_prescaled_fp8qk": [_P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, c_int64_p, _F,
                                 _F, _I, _P, ctypes.c_size_t, _P],
     "cp25_cast_fp8_e4m3": [_P, _I64, _P, _I64, _I64, _I64, _F, _P],
+    "cp25_attn_fwd_prescaled_fp8": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, _F, _F, _I,
+                                    _P, ctypes.c_size_t, _P],
+    "cp25_v_fp8t_bytes": [_I, _I, _I],
+    "cp25_cast_v_fp8t": [_P, c_int64_p, _I, _I, _I, _I, _P, _P, _P],
     "cp25_attn_workspace_bytes": [_I, _I, _I, _I],
     "cp25_attn_plan": [_I, _I, _I, _I, _I],
     "cp25_ln_mod": [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _P, _P, _I64, _I, _I, _I64, _I64, _F, _P],
@@ -106,7 +110,7 @@ def load_library() -> ctypes.CDLL:
             raise RuntimeError(f"libcp25.so does not export {name}")
         if argtypes is not None:
             fn.argtypes = argtypes
-        fn.restype = {"cp25_attn_workspace_bytes": ctypes.c_size_t,
+        fn.restype = {"cp25_attn_workspace_bytes": ctypes.c_size_t, "cp25_v_fp8t_bytes": ctypes.c_int64,
                       "cp25_vae_attn_workspace_bytes": ctypes.c_int64}.get(name, ctypes.c_int)
     _lib = lib
     return lib
@@ -151,7 +155,8 @@ def attn_plan(B: int, H: int, Lq: int, Lk: int, D: int = 128) -> int:
 def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[torch.Tensor] = None,
              softmax_scale: Optional[float] = None, n_split: Optional[int] = None,
              norm_bounds: Optional[Tuple[float, float]] = None, prescaled: bool = False,
-             fp8_qk: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+             fp8_qk: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+             fp8_v: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
     """softmax(q k^T * scale) v for q [B, Lq, H, 128], k/v [B, Lk, H, 128] (bf16, any strides with
     a contiguous head dim). Returns [B, Lq, H, 128] bf16. n_split: key-range split (None = the
     library's plan for this shape; the fp32 partials live in a caching-allocator workspace).
@@ -161,7 +166,8 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
     are those of the scaled q and of k with product <= 60 (cp25_attn_fwd_prescaled; softmax_scale unused).
     fp8_qk=(q8, k8): with prescaled, Q K^T runs on the e4m3 copies (uint8 views shaped like q / k, from
     cast_fp8(q * 2^s), cast_fp8(k * 2^-s); cp25_attn_fwd_prescaled_fp8qk); q / k are then only shape
-    references."""
+    references. fp8_v=(v8t, v_amax) (with fp8_qk; from cast_v_fp8t(v)): P.V on e5m2 P and e4m3 V too
+    (cp25_attn_fwd_prescaled_fp8); v is then only a shape reference."""
     lib = load_library()
     if q.dtype != torch.bfloat16 or k.dtype != torch.bfloat16 or v.dtype != torch.bfloat16:
         raise ValueError("attn_fwd expects bf16 q/k/v (attention() recasts to bf16 first)")
@@ -195,6 +201,16 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
                 raise ValueError("fp8_qk: head dim must be contiguous")
             strides[0] = _i64x3((q8.stride(0), q8.stride(1), q8.stride(2)))
             strides[1] = _i64x3((k8.stride(0), k8.stride(1), k8.stride(2)))
+            if fp8_v is not None:
+                v8t, amax = fp8_v
+                if v8t.dtype != torch.uint8 or v8t.numel() != lib.cp25_v_fp8t_bytes(B, H, Lk) or \
+                        amax.dtype != torch.float32 or amax.numel() < B * H:
+                    raise ValueError("fp8_v: (v8t uint8 of cp25_v_fp8t_bytes, v_amax float32 [B*H]) expected")
+                rc = lib.cp25_attn_fwd_prescaled_fp8(_ptr(q8), _ptr(k8), _ptr(v8t), _ptr(amax), _ptr(out), B, H, Lq, Lk,
+                                                     D, strides[0], strides[1], strides[3], qb, kb, int(n_split),
+                                                     _ptr(ws), ws_bytes, _stream(q.device))
+                _check("cp25_attn_fwd_prescaled_fp8", rc)
+                return out
             rc = lib.cp25_attn_fwd_prescaled_fp8qk(_ptr(q8), _ptr(k8), _ptr(v), _ptr(out), B, H, Lq, Lk, D, *strides,
                                                    qb, kb, int(n_split), _ptr(ws), ws_bytes, _stream(q.device))
             _check("cp25_attn_fwd_prescaled_fp8qk", rc)
@@ -213,6 +229,23 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
     )
     _check("cp25_attn_fwd_bounded", rc)
     return out
+
+
+def cast_v_fp8t(v: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(v8t, v_amax) for attn_fwd(fp8_v=...): v bf16 [B, L, H, 128] (any strides, contiguous head dim) ->
+    the e4m3 V^T tile layout and the per-(b, h) max |v| (cp25_cast_v_fp8t)."""
+    lib = load_library()
+    if v.dtype != torch.bfloat16 or v.dim() != 4 or v.stride(3) != 1:
+        raise ValueError("cast_v_fp8t expects bf16 [B, L, H, 128] with a contiguous head dim")
+    B, L, H, D = v.shape
+    n = lib.cp25_v_fp8t_bytes(B, H, L)
+    _check("cp25_v_fp8t_bytes", min(n, 0))
+    v8t = torch.empty((n,), dtype=torch.uint8, device=v.device)
+    amax = torch.empty((B * H,), dtype=torch.float32, device=v.device)
+    rc = lib.cp25_cast_v_fp8t(_ptr(v), _i64x3((v.stride(0), v.stride(1), v.stride(2))), B, H, L, D, _ptr(v8t),
+                              _ptr(amax), _stream(v.device))
+    _check("cp25_cast_v_fp8t", rc)
+    return v8t, amax
 
 
 def cast_fp8(src: torch.Tensor, scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:

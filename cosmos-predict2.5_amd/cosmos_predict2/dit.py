@@ -207,7 +207,7 @@ class MinimalV1LVGDiT:
         # True: self-attention q rounded to bf16 exactly where the reference rounds it (the scale goes
         # on the fp32 scores); False (default): q * scale * log2(e) rounded once (see _self_attn_mode)
         self.exact_q_rounding = False
-        # "bf16" (default) or "fp8": self-attention Q K^T on e4m3 copies of q and k (set_attention_precision)
+        # "bf16" (default), "fp8qk" (self-attention Q K^T on e4m3) or "fp8" (also P.V on e5m2 P, e4m3 V)
         self.attention_precision = "bf16"
         # the CFG pair's shared block-0 prefix runs once (see _blocks); False: every entry computes it
         self.share_cfg_block0 = True
@@ -225,23 +225,30 @@ class MinimalV1LVGDiT:
         self._fp8_w = {}
 
     def set_attention_precision(self, precision: str) -> None:
-        """"bf16" (default, the reference's arithmetic) or "fp8": where the prescaled form applies, the
-        self-attention's Q K^T runs on v_mfma_f32_32x32x64_f8f6f4 over e4m3 copies of q * 4 and k / 4
-        (cp25_cast_fp8_e4m3, power-of-two scales that cancel in the scores; cp25_attn_fwd_prescaled_fp8qk),
-        P and V stay bf16, the softmax fp32. -18 % on the kernel; e4m3's 3 mantissa bits put ~5 % noise on
-        each score, stated in tests/test_attn_fp8qk_gpu.py. No reference counterpart (config 5's option)."""
-        if precision not in ("bf16", "fp8"):
-            raise ValueError(f"attention precision must be 'bf16' or 'fp8', got {precision!r}")
+        """"bf16" (default, the reference's arithmetic), "fp8qk" or "fp8" (config 5's option; no reference
+        counterpart). Where the prescaled form applies, "fp8qk" runs the self-attention's Q K^T on
+        v_mfma_f32_32x32x64_f8f6f4 over e4m3 copies of q * 4 and k / 4 (cp25_cast_fp8_e4m3, power-of-two scales
+        that cancel in the scores; cp25_attn_fwd_prescaled_fp8qk), P and V bf16: -18 % on the kernel. "fp8"
+        also runs P.V in fp8 (cp25_attn_fwd_prescaled_fp8: P = exp2(S - shift) as e5m2, V as e4m3 with a
+        per-head scale, cp25_cast_v_fp8t): -38 %. The softmax stays fp32. The cost at full depth is stated in
+        tests/test_parity_depth_gpu.py::test_full_depth_2b_forward_fp8_modes."""
+        if precision not in ("bf16", "fp8qk", "fp8"):
+            raise ValueError(f"attention precision must be 'bf16', 'fp8qk' or 'fp8', got {precision!r}")
         self.attention_precision = precision
 
-    def _fp8_qk(self, q_cols: torch.Tensor, k_cols: torch.Tensor, B: int, H: int, hd: int, attn_kw: dict):
-        """attn_fwd kwargs for the fp8 Q K^T form: e4m3 [n, B, H, hd] copies of the q / k columns (2-D row
-        views of the token-major qkv / gathered kv buffers), transposed like the bf16 views."""
-        if self.attention_precision != "fp8" or not attn_kw.get("prescaled"):
+    def _fp8_qk(self, q_cols: torch.Tensor, k_cols: torch.Tensor, B: int, H: int, hd: int, attn_kw: dict,
+                v: Optional[torch.Tensor] = None):
+        """attn_fwd kwargs for the fp8 forms: e4m3 [n, B, H, hd] copies of the q / k columns (2-D row views of
+        the token-major qkv / gathered kv buffers), transposed like the bf16 views; "fp8" also the e4m3 V^T
+        tiles of v ([B, L, H, hd] view)."""
+        if self.attention_precision == "bf16" or not attn_kw.get("prescaled"):
             return attn_kw
         q8 = N.cast_fp8(q_cols, 4.0).view(-1, B, H, hd).transpose(0, 1)
         k8 = N.cast_fp8(k_cols, 0.25).view(-1, B, H, hd).transpose(0, 1)
-        return dict(attn_kw, fp8_qk=(q8, k8))
+        kw = dict(attn_kw, fp8_qk=(q8, k8))
+        if self.attention_precision == "fp8":
+            kw["fp8_v"] = N.cast_v_fp8t(v)
+        return kw
 
     def _self_attn_mode(self, i: int, hd: int):
         """(q out_scale, attn_fwd kwargs) of block i's self-attention. When the norm bound allows
@@ -606,7 +613,7 @@ class MinimalV1LVGDiT:
                     q = qkv.view(n, Bs, 3 * D)[:, :, :D].view(n, Bs, H, hd).transpose(0, 1)
                     kk = qkv.view(n, Bs, 3 * D)[:, :, D:2 * D].view(n, Bs, H, hd).transpose(0, 1)
                     vv = qkv.view(n, Bs, 3 * D)[:, :, 2 * D:].view(n, Bs, H, hd).transpose(0, 1)
-                    attn_kw = self._fp8_qk(qkv[:, :D], qkv[:, D:2 * D], Bs, H, hd, attn_kw)
+                    attn_kw = self._fp8_qk(qkv[:, :D], qkv[:, D:2 * D], Bs, H, hd, attn_kw, vv)
                     if ev is not None:
                         ev[0].record()
                     N.attn_fwd(q, kk, vv, out=o.view(n, Bs, H, hd).transpose(0, 1), **attn_kw)
@@ -705,10 +712,10 @@ class MinimalV1LVGDiT:
         N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=0, weight=p[pre + "self_attn.q_norm.weight"],
                             cos=cos, sin=sin, out_scale=q_scale)
         work.wait()
-        attn_kw = self._fp8_qk(qkv[:, :D], kv_all[:, :D], B, H, hd, attn_kw)
+        kc, vc = kv_chunk_views(kv_all, cp_size * n, B, H, hd)
+        attn_kw = self._fp8_qk(qkv[:, :D], kv_all[:, :D], B, H, hd, attn_kw, vc)
         if e0 is not None:
             e0.record()
-        kc, vc = kv_chunk_views(kv_all, cp_size * n, B, H, hd)
         q = qkv.view(n, B, 3 * D)[:, :, :D].view(n, B, H, hd).transpose(0, 1)
         # the library's key-range split plan: B = 1 launches at CP = 8 leave a ragged last round
         N.attn_fwd(q, kc, vc, out=o.view(n, B, H, hd).transpose(0, 1), **attn_kw)

@@ -109,8 +109,8 @@ class Video2WorldInference:
                  net_cfg: Optional[DiTConfig] = None, sampler_cfg: Optional[SamplerConfig] = None,
                  weights_seed: int = 0, linear_precision: str = "bf16", attention_precision: str = "bf16"):
         """linear_precision: "bf16" (the reference's arithmetic) or "fp8" (the DiT block GEMMs as fp8
-        MFMA, config 5's option; MinimalV1LVGDiT.set_linear_precision). attention_precision: "bf16" or
-        "fp8" (self-attention Q K^T on e4m3 operands; MinimalV1LVGDiT.set_attention_precision)."""
+        MFMA, config 5's option; MinimalV1LVGDiT.set_linear_precision). attention_precision: "bf16", "fp8qk"
+        (self-attention Q K^T on e4m3) or "fp8" (also P.V; MinimalV1LVGDiT.set_attention_precision)."""
         if device is None:
             device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
         self.device = torch.device(device)

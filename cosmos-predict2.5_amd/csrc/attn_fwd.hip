@@ -91,6 +91,9 @@ struct AttnArgs {
   int nsplit;       // key-range splits per (b, h, query block) (1: O written directly)
   int tps;          // key tiles per split
   int nchunk;       // persistent short-KV form: workgroups per (b, h), each a contiguous run of query blocks
+  int ntk_v;        // fp8 P.V: key tiles per (b, h) of the v8t layout (ceil(Lk / 64))
+  const float* v_amax;  // fp8 P.V: per-(b, h) max |v| (v8t holds v * 448 / amax)
+  float s_init;     // fp8 P.V: the Q K^T chains' initial C (-shift: P = exp2(S - shift) <= 2^15 fits e5m2)
   float* o_part;    // nsplit > 1: [nsplit][B][H][Lq][128] fp32 partial O (normalised per split)
   float* lse_part;  // nsplit > 1: [nsplit][B][H][Lq] fp32 log2-sum-exp2 of the scaled scores
   float scale_log2; // softmax scale * log2(e)
@@ -128,17 +131,20 @@ struct AttnArgs {
 // V(t-1) (last read in 2t-1).
 // kKind 0: self-attention, 1: cross-attention (separate symbols in profiles); kFixed: bounded shift;
 // kPre: q pre-scaled by scale * log2(e) and |q| |k| <= kTop (host-checked): P = exp2(S), shift 0
-// kF8 (cp25_attn_fwd_prescaled_fp8qk, the config-5 fp8 option): q and k arrive as OCP e4m3 (bytes, strides in
-// bytes) and S^T = K Q^T runs on v_mfma_f32_32x32x64_f8f6f4: 4 MFMAs of 64 k per tile instead of 16 of 16,
-// K tiles of 64 rows x 128 B (LDS rows 144 B). P and V stay bf16. The operand k order only has to agree between
-// A and B: lane half h, byte i of both operands is d = 64 s + 32 h + i.
+// kF8 >= 1 (cp25_attn_fwd_prescaled_fp8qk, the config-5 fp8 option): q and k arrive as OCP e4m3 (bytes, strides
+// in bytes) and S^T = K Q^T runs on v_mfma_f32_32x32x64_f8f6f4: 4 MFMAs of 64 k per tile instead of 16 of 16,
+// K tiles of 64 rows x 128 B (LDS rows 144 B). The operand k order only has to agree between A and B: lane half
+// h, byte i of both operands is d = 64 s + 32 h + i. kF8 = 2 (cp25_attn_fwd_prescaled_fp8) also runs O^T += V^T
+// P^T there: P as e5m2 straight from the S^T accumulator (byte j = 16 kt + r), V^T as e4m3 from the v8t layout
+// (cp25_cast_v_fp8t: per-(b, h) scale, keys permuted to the P bytes), 4 MFMAs per tile instead of 16, LDS V rows
+// of 64 B padded to 80. The shift that keeps P = exp2(S - shift) <= 2^15 enters as the Q K^T chains' initial C.
 // kPersist (cross-attention, Lk <= 1024, cp25_attn_fwd_prescaled): one workgroup per CU runs a contiguous run of
 // query blocks of one (b, h) as one stream of key tiles (tile t = key tile t % ntk of block t / ntk). The
 // pipeline never drains between blocks: after the MFMA phase that closes a block, the wave stores that block's
 // O (and zeroes it) in its next VALU phase, and Q of the next block is reloaded right after the phase that ran
 // the old Q's last Q K^T. Without it, the 8 key tiles of a 512-key cross-attention paid the whole per-workgroup
 // prologue / epilogue (about 44 tiles of fixed cost, plan_split's fitted model) for every 256 queries.
-template <int kKind, bool kFixed, bool kPre = false, bool kF8 = false, bool kPersist = false>
+template <int kKind, bool kFixed, bool kPre = false, int kF8 = 0, bool kPersist = false>
 __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
   static_assert(!kF8 || kPre, "the fp8 Q K^T form is the prescaled one");
@@ -170,7 +176,8 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   constexpr int QKE = kF8 ? 1 : 2;  // bytes per q / k element
   const char* qp = (const char*)a.q + (b * a.q_sb + h * a.q_sh) * QKE;
   const char* kp = (const char*)a.k + (b * a.k_sb + h * a.k_sh + (int64_t)key0 * a.k_sl) * QKE;
-  const unsigned short* vp = a.v + b * a.v_sb + h * a.v_sh + (int64_t)key0 * a.v_sl;
+  const unsigned short* vp = kF8 == 2 ? (const unsigned short*)((const char*)a.v + ((int64_t)bh * a.ntk_v + key0 / kKBlk) * 8192)
+                                      : a.v + b * a.v_sb + h * a.v_sh + (int64_t)key0 * a.v_sl;
 
   // ---- Q fragments (B operand of S^T = K Q^T): Q[q][16s + 8hl .. +7], s = 0..7 ----
   const int q_row = qb * kQBlk + wave * kQRows + l31;
@@ -222,28 +229,32 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   // offset is loop-invariant, rows past Lk fall outside the descriptor's range and read as zero
   // (their scores are masked to -inf).
   // kF8: a K tile is 64 rows x 128 B, 2 chunks of 16 B per thread of group B (rows u/8 + 32 i, chunk u%8)
+  // kF8 == 2: a V tile is 128 d rows x 64 B (8 KiB contiguous in v8t), 2 chunks per thread of group A (rows u/4 +
+  // 64 i, chunk u%4); always whole (v8t pads the last tile with zero keys)
   const int u = tid & (kThreads / 2 - 1);
   const bool kf8 = kF8 && group_b;
-  const int srow = kf8 ? u >> 3 : u >> 4, sch = kf8 ? u & 7 : u & 15;
-  const int64_t sl = group_b ? a.k_sl : a.v_sl;
-  const int esz = kf8 ? 1 : 2;
+  const bool v8 = kF8 == 2 && !group_b;
+  const int srow = kf8 ? u >> 3 : (v8 ? u >> 2 : u >> 4), sch = kf8 ? u & 7 : (v8 ? u & 3 : u & 15);
+  const int64_t sl = group_b ? a.k_sl : (v8 ? 64 : a.v_sl);
+  const int esz = (kf8 || v8) ? 1 : 2;
   const char* sbase = group_b ? kp : (const char*)vp;
-  const int st_off = (int)(srow * sl * esz) + sch * 16, st_step = (int)((kf8 ? 32 : 16) * sl * esz);
-  const int nst = kf8 ? 2 : 4;
+  const int st_off = (int)(srow * sl * esz) + sch * 16, st_step = (int)((kf8 ? 32 : (v8 ? 64 : 16)) * sl * esz);
+  const int nst = (kf8 || v8) ? 2 : 4;
   u32x4 st[4];
   auto load_tile = [&](int tt) __attribute__((always_inline)) {
     const int t = kPersist ? tt % ntk : tt;
     const int rows = min(Lk - t * kKBlk, kKBlk);
-    const int nbytes = rows > 0 ? (int)((rows - 1) * sl * esz) + esz * kD : 0;
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(sbase + (int64_t)t * kKBlk * sl * esz), (short)0,
-                                                        nbytes, 0x00020000);
+    const int nbytes = v8 ? (rows > 0 ? 8192 : 0) : (rows > 0 ? (int)((rows - 1) * sl * esz) + esz * kD : 0);
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(sbase + (int64_t)t * (v8 ? 8192 : kKBlk * sl * esz)), (short)0, nbytes, 0x00020000);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       if (i < nst)
         st[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, st_off + i * st_step, 0, 0));
   };
   char* const k_wr = smem + srow * KSTR + sch * 16;
-  char* const v_wr = smem + srow * kVStride + sch * 16;
+  constexpr int VSTR8 = 80;  // kF8 == 2: LDS V^T row stride (64 B + 16: conflict-free ds_read_b128 of d rows)
+  char* const v_wr = smem + srow * (kF8 == 2 ? VSTR8 : kVStride) + sch * 16;
   auto write_k = [&](auto BUF) __attribute__((always_inline)) {
     constexpr int kb = decltype(BUF)::value ? KB1 : 0;
     if constexpr (kF8) {
@@ -256,8 +267,13 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   };
   auto write_v = [&](auto BUF) __attribute__((always_inline)) {
     constexpr int vb = decltype(BUF)::value ? VB1 : VB0;
+    if constexpr (kF8 == 2) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(v_wr + vb + 16 * i * kVStride) = st[i];
+      for (int i = 0; i < 2; ++i) *reinterpret_cast<u32x4*>(v_wr + vb + 64 * i * VSTR8) = st[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(v_wr + vb + 16 * i * kVStride) = st[i];
+    }
   };
 
   // per-lane LDS read bases (everything else is an immediate offset)
@@ -274,7 +290,18 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
 
   f32x16 S[2];   // S^T of the tile awaiting its softmax
   bf16x8 pb[4];  // P^T of the tile awaiting its P.V
+  i32x8 pb8;     // kF8 == 2: the same as e5m2 bytes (byte j = P from S[j >> 4][j & 15])
   const f32x16 zero16 = {};
+  f32x16 sinit;  // kF8 == 2: -shift in every element (initial C of the Q K^T chains)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) sinit[r] = kF8 == 2 ? a.s_init : 0.f;
+  // kF8 == 2: one V^T A fragment = 32 B of the d row 32 db + l31, bytes 32 hl .. (two ds_read_b128)
+  const char* const v_rd8 = smem + VB0 + l31 * VSTR8 + 32 * hl;
+  auto v_frag8 = [&](int vb, int db) __attribute__((always_inline)) {
+    const u32x4 lo = *reinterpret_cast<const u32x4*>(v_rd8 + vb + 32 * db * VSTR8);
+    const u32x4 hi = *reinterpret_cast<const u32x4*>(v_rd8 + vb + 32 * db * VSTR8 + 16);
+    return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+  };
 
   // S^T = K Q^T on the K buffer; the first MFMA of each chain takes an inline-constant zero C
   // fp8 form: one A fragment = 32 B of a K row (d 64 s + 32 hl ..), two ds_read_b128
@@ -290,7 +317,8 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
-          S[kt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(k_frag8(kb, kt, s), qf8[s], s == 0 ? zero16 : S[kt],
+          S[kt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(k_frag8(kb, kt, s), qf8[s],
+                                                                 s == 0 ? (kF8 == 2 ? sinit : zero16) : S[kt],
                                                                  0, 0, 0, 0, 0, 0);
       return;
     }
@@ -362,6 +390,22 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
       }
     }
     float psum = 0.f;
+    if constexpr (kF8 == 2) {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        float p[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          p[e] = __builtin_amdgcn_exp2f(S[w >> 2][4 * (w & 3) + e]);
+          psum += p[e];
+        }
+        int q = __builtin_amdgcn_cvt_pk_bf8_f32(p[0], p[1], 0, false);
+        pb8[w] = __builtin_amdgcn_cvt_pk_bf8_f32(p[2], p[3], q, true);
+      }
+      l_run += psum;
+      asm volatile("" ::"v"(pb8), "v"(l_run));
+      return;
+    }
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -496,8 +540,19 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
-          S[kt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(k_frag8(kb, kt, s), qf8[s], s == 0 ? zero16 : S[kt],
+          S[kt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(k_frag8(kb, kt, s), qf8[s],
+                                                                 s == 0 ? (kF8 == 2 ? sinit : zero16) : S[kt],
                                                                  0, 0, 0, 0, 0, 0);
+      if constexpr (kF8 == 2) {
+        // P.V(t) on fp8: A = V^T (e4m3, cbsz 0), B = P^T (e5m2, blgp 1)
+        constexpr int vbb = par ? kVBuf : 0;
+#pragma unroll
+        for (int db = 0; db < 4; ++db)
+          o[db] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(v_frag8(vbb, db), pb8, o[db], 0, 1, 0, 0, 0, 0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_setprio(0);
+        return;
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     static_for<4>(issue);
@@ -571,7 +626,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   if constexpr (kPersist) return;  // every block was stored at its boundary
   // ---- epilogue: O = O^T / l, bf16, row q, d = 32db + 8g + 4hl + (0..3) ----
   const float l_tot = wave_swap_sum(l_run);
-  const float inv = 1.f / l_tot;
+  const float inv = kF8 == 2 ? fmaxf(a.v_amax[bh], 0x1p-100f) * (1.f / 448.f) / l_tot : 1.f / l_tot;
   if (a.nsplit > 1) {
     // partial O of this key range (fp32, normalised by its own sum) + its log2-sum-exp2; merged by
     // attn_merge_splits
@@ -1161,9 +1216,12 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
                        const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
                        const int64_t* o_strides, float softmax_scale, float q_norm_bound, float k_norm_bound,
                        int n_split, void* workspace, size_t ws_bytes, hipStream_t stream, bool prescaled = false,
-                       bool fp8qk = false) {
+                       int fp8 = 0, const float* v_amax = nullptr) {
+  // fp8: 1 = Q K^T on e4m3 q / k; 2 = also P.V on e5m2 P and the e4m3 v8t layout (v = v8t, v_strides unused)
+  const bool fp8qk = fp8 >= 1;
   if (D != kD) return CP25_ERR_DTYPE;
   if (fp8qk && !prescaled) return CP25_ERR_INVAL;
+  if (fp8 == 2 && (!v_amax || ((uintptr_t)v_amax & 3))) return CP25_ERR_INVAL;
   if (prescaled && !(q_norm_bound > 0.f && k_norm_bound > 0.f && (double)q_norm_bound * k_norm_bound <= (double)kTop))
     return CP25_ERR_INVAL;
   if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0) return CP25_ERR_INVAL;
@@ -1175,11 +1233,12 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
   const int64_t* ss[4] = {q_strides, k_strides, v_strides, o_strides};
   for (int i = 0; i < 4; ++i)
     for (int j = 0; j < 3; ++j)
-      if (ss[i][j] % (fp8qk && i < 2 ? 16 : 8) != 0) return CP25_ERR_INVAL;  // 16 B in elements of the operand
+      if (!(fp8 == 2 && i == 2) && ss[i][j] % (fp8qk && i < 2 ? 16 : 8) != 0) return CP25_ERR_INVAL;  // 16 B rows
   // buffer_load offsets within a 64-key tile are 32-bit
-  if ((int64_t)kKBlk * k_strides[1] * (fp8qk ? 1 : 2) >= (1ll << 31) || (int64_t)kKBlk * v_strides[1] * 2 >= (1ll << 31))
+  if ((int64_t)kKBlk * k_strides[1] * (fp8qk ? 1 : 2) >= (1ll << 31) ||
+      (fp8 != 2 && (int64_t)kKBlk * v_strides[1] * 2 >= (1ll << 31)))
     return CP25_ERR_INVAL;
-  if (k_strides[1] <= 0 || v_strides[1] <= 0) return CP25_ERR_INVAL;
+  if (k_strides[1] <= 0 || (fp8 != 2 && v_strides[1] <= 0)) return CP25_ERR_INVAL;
   if (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) & 15) return CP25_ERR_INVAL;
   const int64_t ntiles = cdiv(Lk, kKBlk);
   if (n_split < 1 || n_split > ntiles) return CP25_ERR_INVAL;
@@ -1202,6 +1261,10 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
   a.nsplit = n_split;
   a.tps = (int)tps;
   a.nchunk = 1;
+  a.ntk_v = (int)ntiles;
+  a.v_amax = v_amax;
+  // fp8 P.V: P = exp2(S - shift) <= 2^15 (e5m2 max 57344 = 2^15.8) for every score the norm bounds allow
+  a.s_init = -std::max(0.f, q_norm_bound * k_norm_bound - 15.f);
   a.o_part = n_split > 1 ? (float*)workspace : nullptr;
   a.lse_part = n_split > 1 ? (float*)workspace + (size_t)n_split * rows * kD : nullptr;
   a.scale_log2 = softmax_scale * 1.4426950408889634f;
@@ -1214,8 +1277,11 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
 #endif
   const int64_t nwg = (int64_t)a.nqb * B * H * n_split;
   if (nwg > 0x7fffffff) return CP25_ERR_INVAL;
-  if (fp8qk) {
-    auto kernel = Lk <= 4096 ? attn_fwd_d128<1, true, true, true> : attn_fwd_d128<0, true, true, true>;
+  if (fp8 == 2) {
+    auto kernel = Lk <= 4096 ? attn_fwd_d128<1, true, true, 2> : attn_fwd_d128<0, true, true, 2>;
+    hipLaunchKernelGGL(kernel, dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
+  } else if (fp8qk) {
+    auto kernel = Lk <= 4096 ? attn_fwd_d128<1, true, true, 1> : attn_fwd_d128<0, true, true, 1>;
     hipLaunchKernelGGL(kernel, dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
   } else if ((prescaled || fixed) && use_1w()) {
     const bool dma = attn_variant() == 2;
@@ -1254,7 +1320,17 @@ extern "C" int cp25_attn_fwd_prescaled_fp8qk(const void* q8, const void* k8, con
                                              const int64_t* o_strides, float q_norm_bound, float k_norm_bound,
                                              int n_split, void* workspace, size_t ws_bytes, hipStream_t stream) {
   return attn_launch(q8, k8, v, o, B, H, Lq, Lk, D, q_strides, k_strides, v_strides, o_strides, 0.6931471805599453f,
-                     q_norm_bound, k_norm_bound, n_split, workspace, ws_bytes, stream, true, true);
+                     q_norm_bound, k_norm_bound, n_split, workspace, ws_bytes, stream, true, 1);
+}
+
+extern "C" int cp25_attn_fwd_prescaled_fp8(const void* q8, const void* k8, const void* v8t, const float* v_amax,
+                                           void* o, int B, int H, int Lq, int Lk, int D, const int64_t* q_strides,
+                                           const int64_t* k_strides, const int64_t* o_strides, float q_norm_bound,
+                                           float k_norm_bound, int n_split, void* workspace, size_t ws_bytes,
+                                           hipStream_t stream) {
+  const int64_t none[3] = {0, 0, 0};
+  return attn_launch(q8, k8, v8t, o, B, H, Lq, Lk, D, q_strides, k_strides, none, o_strides, 0.6931471805599453f,
+                     q_norm_bound, k_norm_bound, n_split, workspace, ws_bytes, stream, true, 2, v_amax);
 }
 
 extern "C" size_t cp25_attn_workspace_bytes(int B, int H, int Lq, int n_split) {

@@ -161,7 +161,108 @@ __global__ void __launch_bounds__(256) cast_fp8_kernel(const unsigned short* __r
   *reinterpret_cast<u32x4*>(dst + r * dst_stride + c) = o;
 }
 
+// ---- V for the fp8 P.V of cp25_attn_fwd_prescaled_fp8: per-(b, h) amax, then an e4m3 copy laid out as the MFMA's
+// A operand wants it. v_mfma_f32_32x32x64_f8f6f4 with A = V^T (32 d rows x 64 keys) and B = P^T (64 keys x 32
+// queries): lane half hl, byte j of both operands must name the same key. The P^T operand is the S^T accumulator
+// as it lies in the lane (S[kt][r]: key 32 kt + (r & 3) + 8 (r >> 2) + 4 hl, byte j = 16 kt + r), so a V^T row d
+// of a 64-key tile is stored as 64 bytes p = 32 hl + j holding V[key(j, hl)][d] / scale: v8t[b][h][tile][d][p].
+// One lane then reads its 32-byte fragment contiguously (two ds_read_b128). Keys past L are zero.
+__device__ __forceinline__ int vt_key(int p) {
+  const int hl = p >> 5, j = p & 31;
+  return 32 * (j >> 4) + (j & 3) + 8 * ((j >> 2) & 3) + 4 * hl;
+}
+
+// amax[b * H + h] = max |v| over the L rows of head (b, h) (float bits, atomicMax on non-negative floats as uints).
+// grid (B * H, nchunk), 256 threads: thread t reads 16-B chunk t % 16 of rows t / 16 + 16 i.
+__global__ void __launch_bounds__(256) v_amax_kernel(const unsigned short* __restrict__ v, int64_t sb, int64_t sl,
+                                                     int64_t sh, int H, int L, int rows_per_chunk,
+                                                     unsigned* __restrict__ amax) {
+  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const unsigned short* vp = v + b * sb + h * sh;
+  const int r0 = blockIdx.y * rows_per_chunk, r1 = min(L, r0 + rows_per_chunk);
+  float m = 0.f;
+  for (int r = r0 + (threadIdx.x >> 4); r < r1; r += 16) {
+    const u32x4 w = *reinterpret_cast<const u32x4*>(vp + (int64_t)r * sl + 8 * (threadIdx.x & 15));
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      m = fmaxf(m, fmaxf(fabsf(__uint_as_float(w[e] << 16)), fabsf(__uint_as_float(w[e] & 0xffff0000u))));
+  }
+  m = wave_max(m);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    atomicMax(amax + bh, __float_as_uint(m));
+  }
+}
+
+// v8t tile (b, h, tile): 64 keys x 128 d bf16 through LDS, out as [128 d][64 p] e4m3 of v / scale,
+// scale = max(amax, 2^-100) / 448 (also what the attention multiplies O by). grid (B * H, ntile), 256 threads.
+__global__ void __launch_bounds__(256) v_cast_t_kernel(const unsigned short* __restrict__ v, int64_t sb, int64_t sl,
+                                                       int64_t sh, int H, int L, int ntile,
+                                                       const unsigned* __restrict__ amax,
+                                                       unsigned char* __restrict__ v8t) {
+  constexpr int RS = 128 + 8;  // LDS row stride (bf16 elements)
+  __shared__ unsigned short t[64 * RS];
+  const int bh = blockIdx.x, b = bh / H, h = bh % H, tile = blockIdx.y;
+  const unsigned short* vp = v + b * sb + h * sh;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // 1024 chunks of 8 bf16: key c / 16, d 8 (c % 16)
+    const int c = threadIdx.x + 256 * i, key = c >> 4, d0 = 8 * (c & 15), row = 64 * tile + key;
+    u32x4 w = {0u, 0u, 0u, 0u};
+    if (row < L) w = *reinterpret_cast<const u32x4*>(vp + (int64_t)row * sl + d0);
+    *reinterpret_cast<u32x4*>(t + key * RS + d0) = w;
+  }
+  __syncthreads();
+  const float inv = 448.f / fmaxf(__uint_as_float(amax[bh]), 0x1p-100f);
+  unsigned char* out = v8t + ((int64_t)bh * ntile + tile) * 8192;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // 512 output chunks of 16 B: d = c / 4, p0 = 16 (c % 4)
+    const int c = threadIdx.x + 256 * i, d = c >> 2, p0 = 16 * (c & 3);
+    u32x4 o;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      float f[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const unsigned short x = t[vt_key(p0 + 4 * w + e) * RS + d];
+        f[e] = fminf(fmaxf(__uint_as_float((unsigned)x << 16) * inv, -kFp8Max), kFp8Max);
+      }
+      int q = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+      q = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], q, true);
+      o[w] = (unsigned)q;
+    }
+    *reinterpret_cast<u32x4*>(out + d * 64 + p0) = o;
+  }
+}
+
 }  // namespace
+
+extern "C" int64_t cp25_v_fp8t_bytes(int B, int H, int L) {
+  if (B <= 0 || H <= 0 || L <= 0) return CP25_ERR_INVAL;
+  return (int64_t)B * H * cdiv(L, 64) * 8192;
+}
+
+extern "C" int cp25_cast_v_fp8t(const void* v, const int64_t* v_strides, int B, int H, int L, int D, void* v8t,
+                                float* v_amax, hipStream_t stream) {
+  if (!v || !v_strides || !v8t || !v_amax || B <= 0 || H <= 0 || L <= 0) return CP25_ERR_INVAL;
+  if (D != 128) return CP25_ERR_DTYPE;
+  for (int j = 0; j < 3; ++j)
+    if (v_strides[j] % 8) return CP25_ERR_INVAL;
+  if ((((uintptr_t)v) | ((uintptr_t)v8t)) & 15) return CP25_ERR_INVAL;
+  const int ntile = (int)cdiv(L, 64);
+  unsigned* amax = reinterpret_cast<unsigned*>(v_amax);
+  if (hipMemsetAsync(amax, 0, sizeof(unsigned) * B * H, stream) != hipSuccess) return CP25_ERR_LAUNCH;
+  const int rows_per_chunk = 1024, nchunk = (int)cdiv(L, rows_per_chunk);
+  hipLaunchKernelGGL(v_amax_kernel, dim3(B * H, nchunk), dim3(256), 0, stream, (const unsigned short*)v, v_strides[0],
+                     v_strides[1], v_strides[2], H, L, rows_per_chunk, amax);
+  CP25_LAUNCH_CHECK();
+  hipLaunchKernelGGL(v_cast_t_kernel, dim3(B * H, ntile), dim3(256), 0, stream, (const unsigned short*)v, v_strides[0],
+                     v_strides[1], v_strides[2], H, L, ntile, (const unsigned*)amax, (unsigned char*)v8t);
+  CP25_LAUNCH_CHECK();
+  return CP25_OK;
+}
 
 extern "C" int cp25_cast_fp8_e4m3(const void* src, int64_t src_stride, void* dst, int64_t dst_stride, int64_t n_rows,
                                   int64_t width, float scale, hipStream_t stream) {

@@ -91,6 +91,25 @@ int cp25_attn_fwd_prescaled_fp8qk(const void* q8, const void* k8, const void* v,
                                   const int64_t* o_strides, float q_norm_bound, float k_norm_bound, int n_split,
                                   void* workspace, size_t ws_bytes, hipStream_t stream);
 
+/* V for the fp8 P.V of cp25_attn_fwd_prescaled_fp8: v_amax[b * H + h] = max |v| over the head's L rows (float,
+ * device memory, B * H entries), then v8t = e4m3(v * 448 / amax) laid out [B][H][ceil(L / 64)][128 d][64 key
+ * bytes], the keys of each 64-key tile permuted to the order the kernel's P^T operand holds them (zero keys pad
+ * the last tile). v: bf16 [B, L, H, 128] by element strides (e.g. the v columns of the fused qkv buffer). Two
+ * HBM passes over v, no host synchronisation. cp25_v_fp8t_bytes gives the v8t size. */
+int64_t cp25_v_fp8t_bytes(int B, int H, int L);
+int cp25_cast_v_fp8t(const void* v, const int64_t* v_strides, int B, int H, int L, int D, void* v8t, float* v_amax,
+                     hipStream_t stream);
+
+/* The config-5 fp8 option's whole attention: cp25_attn_fwd_prescaled_fp8qk's e4m3 Q K^T, then O^T += V^T P^T on
+ * v_mfma_f32_32x32x64_f8f6f4 with P = exp2(S - shift) as e5m2 (shift = max(0, q_norm_bound * k_norm_bound - 15)
+ * keeps every P <= 2^15, inside e5m2, whatever the data) and V^T from cp25_cast_v_fp8t's v8t (O rescaled by
+ * amax / 448 at the end). The softmax stays fp32 with no per-score multiply and no running max. o bf16. No
+ * reference counterpart; replaces the same attention call. */
+int cp25_attn_fwd_prescaled_fp8(const void* q8, const void* k8, const void* v8t, const float* v_amax, void* o, int B,
+                                int H, int Lq, int Lk, int D, const int64_t* q_strides, const int64_t* k_strides,
+                                const int64_t* o_strides, float q_norm_bound, float k_norm_bound, int n_split,
+                                void* workspace, size_t ws_bytes, hipStream_t stream);
+
 /* Bytes of workspace cp25_attn_fwd_split / _bounded need (0 for n_split <= 1). */
 size_t cp25_attn_workspace_bytes(int B, int H, int Lq, int n_split);
 

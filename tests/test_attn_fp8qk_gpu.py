@@ -60,3 +60,65 @@ def test_attn_fp8qk_vs_fp32(device, B, H, L, Lk, split):
     # the format's cost: e4m3 rounds each q, k element by up to 2^-4 relative, ~0.05 (natural-log units) of score
     # noise for unit-RMS rows; with random (near-uniform) attention that moves the output by ~5% of its norm
     assert e8 <= 6e-2, e8
+
+
+def _vt_key(p):
+    hl, j = p >> 5, p & 31
+    return 32 * (j >> 4) + (j & 3) + 8 * ((j >> 2) & 3) + 4 * hl
+
+
+def test_cast_v_fp8t_layout_bit_exact(device):
+    """cp25_cast_v_fp8t: per-(b, h) amax exact, and every byte of the permuted V^T tiles equal to torch's e4m3 of
+    v * 448 / amax (keys past L zero), with v a strided view of a token-major buffer."""
+    B, H, L = 2, 3, 200
+    g = torch.Generator().manual_seed(4)
+    buf = (torch.randn(L, B, 3 * H * 128, generator=g) * 2).to(device, torch.bfloat16)
+    v = buf[:, :, 2 * H * 128:].view(L, B, H, 128).transpose(0, 1)
+    v8t, amax = N.cast_v_fp8t(v)
+    vf = v.float()
+    ref_amax = vf.abs().amax(dim=(1, 3)).reshape(B * H)
+    assert torch.equal(amax, ref_amax)
+    nt = (L + 63) // 64
+    perm = torch.tensor([_vt_key(p) for p in range(64)], device=device)
+    vp = torch.zeros(B, nt * 64, H, 128, device=device)
+    vp[:, :L] = vf
+    scaled = vp * (448.0 / ref_amax.view(B, 1, H, 1))
+    tiles = scaled.view(B, nt, 64, H, 128)[:, :, perm]  # [B, nt, 64 p, H, 128 d]
+    ref = tiles.permute(0, 3, 1, 4, 2).clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8)  # [B, H, nt, d, p]
+    assert torch.equal(v8t.view(B, H, nt, 128, 64), ref)
+
+
+@pytest.mark.parametrize("B,H,L,Lk,split", [(1, 2, 1000, 1000, None), (2, 4, 4800, 4800, None),
+                                             (1, 3, 333, 1111, 3), (1, 2, 64, 4097, 5)])
+def test_attn_fp8_full_vs_fp32(device, B, H, L, Lk, split):
+    """cp25_attn_fwd_prescaled_fp8 (e4m3 Q K^T, e5m2 P, e4m3 V): exact against fp32 math on the same quantised
+    operands (P rounded to e5m2 after the launch's shift, V through v8t's per-head scale; the row sums of the
+    unrounded P, as the kernel keeps them), and the format's cost against fp32 on the bf16 inputs."""
+    q = _normed((B, L, H, 128), 1, device)
+    k = _normed((B, Lk, H, 128), 2, device)
+    v = torch.randn((B, Lk, H, 128), device=device, generator=torch.Generator(device=device).manual_seed(3)).to(torch.bfloat16)
+    qs = (q.float() * C).to(torch.bfloat16)
+    nb = (128 ** 0.5 * 1.02 * C, 128 ** 0.5 * 1.02)
+    q8 = N.cast_fp8(qs.reshape(-1, 128), QS).view(B, L, H, 128)
+    k8 = N.cast_fp8(k.reshape(-1, 128), 1.0 / QS).view(B, Lk, H, 128)
+    v8t, amax = N.cast_v_fp8t(v)
+    o8 = N.attn_fwd(qs, k, v, norm_bounds=nb, prescaled=True, fp8_qk=(q8, k8), fp8_v=(v8t, amax), n_split=split)
+    shift = max(0.0, nb[0] * nb[1] - 15.0)
+    qd = q8.view(torch.float8_e4m3fn).float() / QS
+    kd = k8.view(torch.float8_e4m3fn).float() * QS
+    s = torch.einsum("bqhd,bkhd->bhqk", qd, kd) - shift  # log2 units
+    p = torch.exp2(s)
+    p8 = p.to(torch.float8_e5m2).float()
+    sc = (amax / 448.0).view(B, H)
+    vd = ((v.float() / sc.view(B, 1, H, 1)).clamp(-448, 448).to(torch.float8_e4m3fn).float()) * sc.view(B, 1, H, 1)
+    emu = torch.einsum("bhqk,bkhd->bqhd", p8, vd) / p.sum(-1).permute(0, 2, 1)[..., None]
+    s32 = torch.einsum("bqhd,bkhd->bhqk", q.float(), k.float()) * 128 ** -0.5
+    full = torch.einsum("bhqk,bkhd->bqhd", torch.softmax(s32, -1), v.float())
+    rel = lambda o, r: ((o.float() - r).norm() / r.norm()).item()  # noqa: E731
+    e_emu, e_full = rel(o8, emu), rel(o8, full)
+    print(f"fp8 attention B={B} H={H} Lq={L} Lk={Lk} split={split}: vs fp32 on the quantised operands {e_emu:.2e}, "
+          f"vs fp32 {e_full:.2e}")
+    assert torch.isfinite(o8.float()).all()
+    assert e_emu <= 4e-3, e_emu
+    # e5m2 P (2 mantissa bits) + e4m3 Q K^T + e4m3 V on random, near-uniform attention
+    assert e_full <= 1e-1, e_full

@@ -12,7 +12,9 @@ match the single-rank run (guidance 0, 2 Karras steps = 3 evals x CFG).
   batch 1 vs 2 and split vs unsplit attention round differently (~1 bf16 ulp per GEMM output,
   ~2e-3 per forward), amplified over 3 evaluations: rel-L2 <= 1.5e-2.
 * the fp8 option through the same lanes: activation scales are per token row, so a token shard
-  quantises exactly as the whole sequence does and CP = 2 must again match CP = 1 bit for bit.
+  quantises exactly as the whole sequence does and CP = 2 must again match CP = 1 bit for bit; the
+  fp8 attention too (q / k scales are fixed powers of two, V's per-head scale is taken over the gathered
+  keys, which every rank holds whole).
 """
 import os
 import socket
@@ -57,6 +59,13 @@ def _run(model, gt, cc, cu, shape, dev):
                                 guidance=0.0, seed=0, num_steps=2).cpu()
 
 
+def _set_precision(m, precision):
+    if precision == "fp8attn":
+        m.net.set_attention_precision("fp8")
+    else:
+        m.net.set_linear_precision(precision)
+
+
 def _worker(rank, world, port, q, split_env, precision="bf16"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if split_env:
@@ -69,7 +78,7 @@ def _worker(rank, world, port, q, split_env, precision="bf16"):
         cfg, scfg, sd, gt, cc, cu, shape = _case()
         m = Video2WorldModelRectifiedFlow(cfg, scfg, device=dev)
         m.load_state_dict(sd)
-        m.net.set_linear_precision(precision)
+        _set_precision(m, precision)
         m.set_context_parallel_group(dist.group.WORLD)
         out = _run(m, gt, cc, cu, shape, dev)
         q.put((rank, out.numpy()))  # by value: a shared-memory fd dies with this process
@@ -77,7 +86,8 @@ def _worker(rank, world, port, q, split_env, precision="bf16"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("split_env,tol,precision", [("1", 0.0, "bf16"), ("", 1.5e-2, "bf16"), ("1", 0.0, "fp8")])
+@pytest.mark.parametrize("split_env,tol,precision", [("1", 0.0, "bf16"), ("", 1.5e-2, "bf16"), ("1", 0.0, "fp8"),
+                                                     ("1", 0.0, "fp8attn")])
 def test_cp2_matches_cp1(device, monkeypatch, split_env, tol, precision):
     from cosmos_predict2.model import Video2WorldModelRectifiedFlow
 
@@ -88,7 +98,7 @@ def test_cp2_matches_cp1(device, monkeypatch, split_env, tol, precision):
     cfg, scfg, sd, gt, cc, cu, shape = _case()
     m = Video2WorldModelRectifiedFlow(cfg, scfg, device=device)
     m.load_state_dict(sd)
-    m.net.set_linear_precision(precision)
+    _set_precision(m, precision)
     m.net.force_lanes = bool(split_env)
     ref = _run(m, gt, cc, cu, shape, device)
     del m

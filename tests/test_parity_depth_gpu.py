@@ -96,16 +96,22 @@ def test_full_depth_2b_forward_fp8_modes(device, net2b):
     net.load_state_dict(sd)
     args = (x.to(device).to(torch.bfloat16), t.to(device), ctx.to(device))
     dist, outs = {}, {}
-    for lin, att in (("bf16", "bf16"), ("bf16", "fp8"), ("fp8", "bf16"), ("fp8", "fp8")):
+    modes = (("bf16", "bf16"), ("bf16", "fp8qk"), ("bf16", "fp8"), ("fp8", "bf16"), ("fp8", "fp8"))
+    for lin, att in modes:
         net.set_linear_precision(lin)
         net.set_attention_precision(att)
         outs[(lin, att)] = hip = net(*args, condition_video_input_mask_B_C_T_H_W=mask.to(device)).cpu()
         assert torch.isfinite(hip).all()
         dist[(lin, att)] = _report(f"28-block 2B forward, linear {lin}, attention {att}", hip, ref, truth)
-    # measured (MI355X, round 2): hip-truth bf16/bf16 1.162e-2, bf16/fp8-attention 1.171e-2, fp8/bf16 6.58e-2,
-    # fp8/fp8 6.48e-2 (bf16 reference 1.164e-2): the fp8 Q K^T passes the bf16 path's own gate
-    assert not torch.equal(outs[("bf16", "fp8")], outs[("bf16", "bf16")])  # the fp8 Q K^T really ran
-    assert dist[("bf16", "fp8")]["hip_truth"] <= 1.1 * dist[("bf16", "fp8")]["ref_truth"], dist
+    net.set_linear_precision("bf16")
+    net.set_attention_precision("bf16")
+    # measured (MI355X, round 2): hip-truth bf16/bf16 1.162e-2, bf16/fp8qk 1.171e-2, fp8/bf16 6.58e-2 (bf16
+    # reference 1.164e-2): the fp8 Q K^T passes the bf16 path's own gate; the CPU emulation of the fp8 P.V
+    # (tools/sim_fp8_attention_depth.py) put bf16/fp8 at 1.198e-2
+    for att in ("fp8qk", "fp8"):
+        assert not torch.equal(outs[("bf16", att)], outs[("bf16", "bf16")])  # the fp8 attention really ran
+    assert dist[("bf16", "fp8qk")]["hip_truth"] <= 1.1 * dist[("bf16", "fp8qk")]["ref_truth"], dist
+    assert dist[("bf16", "fp8")]["hip_truth"] <= 1.2 * dist[("bf16", "fp8")]["ref_truth"], dist
     for key in (("fp8", "bf16"), ("fp8", "fp8")):
         assert dist[key]["hip_truth"] <= 7e-2, dist
 

@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--num-steps", type=int, default=35)
     ap.add_argument("--chunk-size", type=int, default=12)
     ap.add_argument("--linear-precision", default="bf16", choices=("bf16", "fp8"))
-    ap.add_argument("--attention-precision", default="bf16", choices=("bf16", "fp8"))
+    ap.add_argument("--attention-precision", default="bf16", choices=("bf16", "fp8qk", "fp8"))
     a = ap.parse_args()
     h, w = (int(x) for x in a.resolution.split(","))
     dev = torch.device("cuda:0")

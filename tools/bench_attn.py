@@ -35,6 +35,8 @@ def main():
                     help="with --bounded: q carries scale*log2(e) (the DiT's default form, cp25_attn_fwd_prescaled)")
     ap.add_argument("--fp8qk", action="store_true",
                     help="with --prescaled: Q K^T on e4m3 copies of q*4 and k/4 (cp25_attn_fwd_prescaled_fp8qk)")
+    ap.add_argument("--fp8pv", action="store_true",
+                    help="with --fp8qk: P.V on e5m2 P and e4m3 V too (cp25_attn_fwd_prescaled_fp8)")
     ap.add_argument("--lib", default="", help="lab build of libcp25.so to load instead of the in-tree one")
     a = ap.parse_args()
     if a.lib:
@@ -74,6 +76,8 @@ def main():
                 q8 = N.cast_fp8(q.reshape(-1, 128), 4.0).view(q.shape)
                 k8 = N.cast_fp8(k.reshape(-1, 128), 0.25).view(k.shape)
             pre["fp8_qk"] = (q8, k8)
+            if a.fp8pv:
+                pre["fp8_v"] = N.cast_v_fp8t(v)
     # correctness of the loaded build on a small shape (ragged length) vs fp32 math
     gc = torch.Generator(device=dev).manual_seed(1)
     qc, kc, vc = (torch.randn(1, 1000, 2, 128, device=dev, generator=gc).to(torch.bfloat16) for _ in range(3))
@@ -96,7 +100,7 @@ def main():
     ms = e0.elapsed_time(e1) / a.iters
     flop = 4.0 * a.B * a.H * a.L * Lk * 128
     print(json.dumps({"kernel": "attn_fwd", "B": a.B, "H": a.H, "Lq": a.L, "Lk": Lk, "fused": a.fused,
-                      "zeros": a.zeros, "bounded": a.bounded, "prescaled": a.prescaled, "fp8qk": a.fp8qk, "normed": a.normed or a.bounded, "split": ns, "iters": a.iters, "lib": os.path.basename(a.lib) or "libcp25.so", "ms": ms,
+                      "zeros": a.zeros, "bounded": a.bounded, "prescaled": a.prescaled, "fp8qk": a.fp8qk, "fp8pv": a.fp8pv, "normed": a.normed or a.bounded, "split": ns, "iters": a.iters, "lib": os.path.basename(a.lib) or "libcp25.so", "ms": ms,
                       "tflops": flop / ms / 1e9, "check_rel_l2": check}))
 
 
