@@ -138,6 +138,9 @@ struct AttnArgs {
 // P^T there: P as e5m2 straight from the S^T accumulator (byte j = 16 kt + r), V^T as e4m3 from the v8t layout
 // (cp25_cast_v_fp8t: per-(b, h) scale, keys permuted to the P bytes), 4 MFMAs per tile instead of 16, LDS V rows
 // of 64 B padded to 80. The shift that keeps P = exp2(S - shift) <= 2^15 enters as the Q K^T chains' initial C.
+// kF8 = 3 makes the e5m2 byte of P without exp2: n = round(4 (S - shift) + 60) clamped to [0, 255] by one
+// v_cvt_pk_u8_f32 (after one fma) is read as e5m2, i.e. 2^(n / 4 - 15) with a linear mantissa, and the row sums
+// come from a fifth P.V MFMA against an all-ones V^T row (so they are the sums of the P actually used).
 // kPersist (cross-attention, Lk <= 1024, cp25_attn_fwd_prescaled): one workgroup per CU runs a contiguous run of
 // query blocks of one (b, h) as one stream of key tiles (tile t = key tile t % ntk of block t / ntk). The
 // pipeline never drains between blocks: after the MFMA phase that closes a block, the wave stores that block's
@@ -149,6 +152,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
   static_assert(!kF8 || kPre, "the fp8 Q K^T form is the prescaled one");
   static_assert(!kPersist || (kPre && !kF8), "the persistent form is the prescaled bf16 one");
+  static_assert(kF8 >= 0 && kF8 <= 3, "kF8: 0 bf16, 1 fp8 Q K^T, 2 + fp8 P.V, 3 + P bytes without exp2");
   constexpr int KSTR = kF8 ? 144 : kKStride;        // K LDS row stride
   constexpr int KB1 = kKBlk * KSTR;                 // K buffer 1
   constexpr int VB0 = 2 * kKBlk * KSTR, VB1 = VB0 + kVBuf;
@@ -176,7 +180,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   constexpr int QKE = kF8 ? 1 : 2;  // bytes per q / k element
   const char* qp = (const char*)a.q + (b * a.q_sb + h * a.q_sh) * QKE;
   const char* kp = (const char*)a.k + (b * a.k_sb + h * a.k_sh + (int64_t)key0 * a.k_sl) * QKE;
-  const unsigned short* vp = kF8 == 2 ? (const unsigned short*)((const char*)a.v + ((int64_t)bh * a.ntk_v + key0 / kKBlk) * 8192)
+  const unsigned short* vp = kF8 >= 2 ? (const unsigned short*)((const char*)a.v + ((int64_t)bh * a.ntk_v + key0 / kKBlk) * 8192)
                                       : a.v + b * a.v_sb + h * a.v_sh + (int64_t)key0 * a.v_sl;
 
   // ---- Q fragments (B operand of S^T = K Q^T): Q[q][16s + 8hl .. +7], s = 0..7 ----
@@ -233,7 +237,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   // 64 i, chunk u%4); always whole (v8t pads the last tile with zero keys)
   const int u = tid & (kThreads / 2 - 1);
   const bool kf8 = kF8 && group_b;
-  const bool v8 = kF8 == 2 && !group_b;
+  const bool v8 = kF8 >= 2 && !group_b;
   const int srow = kf8 ? u >> 3 : (v8 ? u >> 2 : u >> 4), sch = kf8 ? u & 7 : (v8 ? u & 3 : u & 15);
   const int64_t sl = group_b ? a.k_sl : (v8 ? 64 : a.v_sl);
   const int esz = (kf8 || v8) ? 1 : 2;
@@ -254,7 +258,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   };
   char* const k_wr = smem + srow * KSTR + sch * 16;
   constexpr int VSTR8 = 80;  // kF8 == 2: LDS V^T row stride (64 B + 16: conflict-free ds_read_b128 of d rows)
-  char* const v_wr = smem + srow * (kF8 == 2 ? VSTR8 : kVStride) + sch * 16;
+  char* const v_wr = smem + srow * (kF8 >= 2 ? VSTR8 : kVStride) + sch * 16;
   auto write_k = [&](auto BUF) __attribute__((always_inline)) {
     constexpr int kb = decltype(BUF)::value ? KB1 : 0;
     if constexpr (kF8) {
@@ -267,7 +271,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
   };
   auto write_v = [&](auto BUF) __attribute__((always_inline)) {
     constexpr int vb = decltype(BUF)::value ? VB1 : VB0;
-    if constexpr (kF8 == 2) {
+    if constexpr (kF8 >= 2) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) *reinterpret_cast<u32x4*>(v_wr + vb + 64 * i * VSTR8) = st[i];
     } else {
@@ -290,11 +294,14 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
 
   f32x16 S[2];   // S^T of the tile awaiting its softmax
   bf16x8 pb[4];  // P^T of the tile awaiting its P.V
-  i32x8 pb8;     // kF8 == 2: the same as e5m2 bytes (byte j = P from S[j >> 4][j & 15])
+  i32x8 pb8;     // kF8 >= 2: the same as e5m2 bytes (byte j = P from S[j >> 4][j & 15])
   const f32x16 zero16 = {};
-  f32x16 sinit;  // kF8 == 2: -shift in every element (initial C of the Q K^T chains)
+  f32x16 sinit;  // kF8 >= 2: -shift in every element (initial C of the Q K^T chains)
 #pragma unroll
-  for (int r = 0; r < 16; ++r) sinit[r] = kF8 == 2 ? a.s_init : 0.f;
+  for (int r = 0; r < 16; ++r) sinit[r] = kF8 >= 2 ? a.s_init : 0.f;
+  f32x16 lsum = {};  // kF8 == 3: the row sums, from P^T against an all-ones V^T row (every row of the block equal)
+  const i32x8 ones8 = {0x38383838, 0x38383838, 0x38383838, 0x38383838, 0x38383838, 0x38383838, 0x38383838,
+                       0x38383838};  // e4m3 1.0
   // kF8 == 2: one V^T A fragment = 32 B of the d row 32 db + l31, bytes 32 hl .. (two ds_read_b128)
   const char* const v_rd8 = smem + VB0 + l31 * VSTR8 + 32 * hl;
   auto v_frag8 = [&](int vb, int db) __attribute__((always_inline)) {
@@ -318,7 +325,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
           S[kt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(k_frag8(kb, kt, s), qf8[s],
-                                                                 s == 0 ? (kF8 == 2 ? sinit : zero16) : S[kt],
+                                                                 s == 0 ? (kF8 >= 2 ? sinit : zero16) : S[kt],
                                                                  0, 0, 0, 0, 0, 0);
       return;
     }
@@ -390,6 +397,17 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
       }
     }
     float psum = 0.f;
+    if constexpr (kF8 == 3) {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        unsigned x = 0u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x = __builtin_amdgcn_cvt_pk_u8_f32(fmaf(S[w >> 2][4 * (w & 3) + e], 4.f, 60.f), e, x);
+        pb8[w] = (int)x;
+      }
+      asm volatile("" ::"v"(pb8));
+      return;
+    }
     if constexpr (kF8 == 2) {
 #pragma unroll
       for (int w = 0; w < 8; ++w) {
@@ -541,14 +559,15 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
           S[kt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(k_frag8(kb, kt, s), qf8[s],
-                                                                 s == 0 ? (kF8 == 2 ? sinit : zero16) : S[kt],
+                                                                 s == 0 ? (kF8 >= 2 ? sinit : zero16) : S[kt],
                                                                  0, 0, 0, 0, 0, 0);
-      if constexpr (kF8 == 2) {
+      if constexpr (kF8 >= 2) {
         // P.V(t) on fp8: A = V^T (e4m3, cbsz 0), B = P^T (e5m2, blgp 1)
         constexpr int vbb = par ? kVBuf : 0;
 #pragma unroll
         for (int db = 0; db < 4; ++db)
           o[db] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(v_frag8(vbb, db), pb8, o[db], 0, 1, 0, 0, 0, 0);
+        if constexpr (kF8 == 3) lsum = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ones8, pb8, lsum, 0, 1, 0, 0, 0, 0);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_setprio(0);
         return;
@@ -625,8 +644,8 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_d128(AttnArgs a) {
 
   if constexpr (kPersist) return;  // every block was stored at its boundary
   // ---- epilogue: O = O^T / l, bf16, row q, d = 32db + 8g + 4hl + (0..3) ----
-  const float l_tot = wave_swap_sum(l_run);
-  const float inv = kF8 == 2 ? fmaxf(a.v_amax[bh], 0x1p-100f) * (1.f / 448.f) / l_tot : 1.f / l_tot;
+  const float l_tot = kF8 == 3 ? lsum[0] : wave_swap_sum(l_run);
+  const float inv = kF8 >= 2 ? fmaxf(a.v_amax[bh], 0x1p-100f) * (1.f / 448.f) / l_tot : 1.f / l_tot;
   if (a.nsplit > 1) {
     // partial O of this key range (fp32, normalised by its own sum) + its log2-sum-exp2; merged by
     // attn_merge_splits
@@ -1263,8 +1282,9 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
   a.nchunk = 1;
   a.ntk_v = (int)ntiles;
   a.v_amax = v_amax;
-  // fp8 P.V: P = exp2(S - shift) <= 2^15 (e5m2 max 57344 = 2^15.8) for every score the norm bounds allow
-  a.s_init = -std::max(0.f, q_norm_bound * k_norm_bound - 15.f);
+  // fp8 P.V: P = exp2(S - shift) <= 2^15 (e5m2 max 57344 = 2^15.8) for every score the norm bounds allow, with
+  // the e4m3 rounding of q and k (each element within 2^-4 relative: |q8| |k8| <= 1.13 |q| |k|)
+  a.s_init = -std::max(0.f, 1.13f * q_norm_bound * k_norm_bound - 15.f);
   a.o_part = n_split > 1 ? (float*)workspace : nullptr;
   a.lse_part = n_split > 1 ? (float*)workspace + (size_t)n_split * rows * kD : nullptr;
   a.scale_log2 = softmax_scale * 1.4426950408889634f;
@@ -1278,7 +1298,11 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
   const int64_t nwg = (int64_t)a.nqb * B * H * n_split;
   if (nwg > 0x7fffffff) return CP25_ERR_INVAL;
   if (fp8 == 2) {
-    auto kernel = Lk <= 4096 ? attn_fwd_d128<1, true, true, 2> : attn_fwd_d128<0, true, true, 2>;
+    // CP25_F8_EXP=exact: P by exp2 + cvt_pk_bf8 and fp32 row sums (the A/B reference of the integer form)
+    const char* e = getenv("CP25_F8_EXP");
+    const bool exact = e && e[0] == 'e';
+    auto kernel = exact ? (Lk <= 4096 ? attn_fwd_d128<1, true, true, 2> : attn_fwd_d128<0, true, true, 2>)
+                        : (Lk <= 4096 ? attn_fwd_d128<1, true, true, 3> : attn_fwd_d128<0, true, true, 3>);
     hipLaunchKernelGGL(kernel, dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
   } else if (fp8qk) {
     auto kernel = Lk <= 4096 ? attn_fwd_d128<1, true, true, 1> : attn_fwd_d128<0, true, true, 1>;

@@ -8,6 +8,9 @@ each compared with the fp32 truth (the same test geometry and seeds as tests/tes
   pvc  : as qkpv with one constant shift per launch, b = max|q c| max|k| - 15 (what the kernel builds: the shift
          enters as the Q K^T MFMA chain's initial C)
   pv43 : + P as e4m3 with the shift b_row - 8 (P <= 256 < 448) instead: underflows whole rows (NaN)
+  pvs  : as pvc, but the e5m2 byte of P made in one integer convert, n = round(4 (S - shift) + 60) clamped to
+         [0, 123] and read as e5m2 (2^(n/4 - 15) with a linear mantissa: exp2 never evaluated), the row sums
+         taken over those P (an all-ones V^T row in the P.V MFMA)
 
 usage: python tools/sim_fp8_attention_depth.py  (about 10 CPU-minutes)
 """
@@ -42,10 +45,14 @@ def make_sdpa(mode):
             o = (p.to(torch.bfloat16).float() @ vf) / p.sum(-1, keepdim=True)
         else:
             b = qs.transpose(1, 2).norm(dim=-1, keepdim=True) * k.float().norm(dim=-1).amax() * 1.0
-            if mode == "pvc":
+            if mode in ("pvc", "pvs"):
                 b = b.amax()
-            top, fmt = (15.0, E5) if mode in ("qkpv", "pvc") else (8.0, E4)
-            p = torch.exp2(s - (b - top)).to(fmt).float()
+            top, fmt = (15.0, E5) if mode in ("qkpv", "pvc", "pvs") else (8.0, E4)
+            if mode == "pvs":
+                n = torch.round(4 * (s - (b - top)) + 60).clamp(0, 123).to(torch.uint8)
+                p = n.view(E5).float()
+            else:
+                p = torch.exp2(s - (b - top)).to(fmt).float()
             vsc = vf.abs().amax().clamp(min=1e-30) / 448.0
             v8 = (vf / vsc).to(E4).float() * vsc
             o = (p @ v8) / p.sum(-1, keepdim=True)
