@@ -1159,7 +1159,360 @@ __global__ void __launch_bounds__(256) attn_merge_splits(const float* __restrict
   *reinterpret_cast<u16x4*>(o + b * o_sb + (int64_t)q * o_sl + h * o_sh + d) = w;
 }
 
+// ------------------------------------------------------------------------------------------------
+// attn_fwd_m16: the bounded-shift / prescaled kernel on v_mfma_f32_16x16x32_bf16 (the default for those forms).
+// Same workgroup (8 waves x 32 query rows of one (b, h)), the same ping-pong schedule, K/V staging and
+// double-buffered LDS tiles as attn_fwd_d128; only the MFMA shape differs. Why: under sustained MFMA load the
+// chip's clock is set by power, and on random data it holds a higher clock on the 16x16x32 shape than on
+// 32x32x16 at equal cycles per FLOP (MI355X_MICROARCH "DVFS give-back" item 7: 1.12-1.15x in bare loops;
+// cdna_hip_programming §5.4 rule 28), while the d128 kernel already runs at that 32x32x16 loop's rate.
+// Fragments (lane l, g = l >> 4, c = l & 15), per wave and 64-key tile:
+//   S^T = K Q^T: 4 key blocks kb x 2 query halves qh x 4 d-steps s = 32 MFMAs. A = K[16 kb + c][32 s + 8 g ..]
+//     (one ds_read_b128, shared by both qh), B = Q[16 qh + c][32 s + 8 g ..] (32 VGPRs resident), C: lane holds
+//     keys 16 kb + 4 g + i (i < 4) of query 16 qh + c: every lane owns two query rows and 16 keys of each.
+//   O^T = V^T P^T: 8 d blocks db x 2 qh x 2 key steps ks = 32 MFMAs. B = P^T packed lane-locally from the two S
+//     blocks kb = 2 ks, 2 ks + 1 (k slot 8 g + j <-> key 32 ks + 16 (j >> 2) + 4 g + (j & 3)); A = V^T in that
+//     same key order: two ds_read_b64_tr_b16 (rows 32 ks + 4 g + q and 32 ks + 16 + 4 g + q, columns 16 db + 4 p
+//     for lane 16 g + 4 q + p), shared by both qh.
+// A query row's sum is spread over the 4 lane groups; with the fixed shift nothing needs it before the epilogue
+// (one cross-group reduction per row). LDS rows of 288 B (256 + 32) for both K and V: a ds_read_b128 of the K
+// fragment is serviced in the four 16-lane groups {0-3, 12-15, 20-27}, {4-11, 16-19, 28-31}, ... (MI355X_MICROARCH
+// §LDS), which mix rows c = 0..15 of lane groups g and g + 1; at 288 B the 16-B slot is (2 c + g + 4 s) mod 16,
+// distinct within every such group (the d128 kernel's 272 B gives (c + g) mod 16: one 2-way conflict per group and
+// read, measured 64 extra LDS cycles per wave and tile). The transposed V reads (two 32-lane halves, 8 rows x 32
+// B each) land on 8 distinct 32-B bank groups.
+constexpr int kKStride16 = 288;
+constexpr int kVStride16 = 288;
+#ifndef CP25_M16_AHEAD
+#define CP25_M16_AHEAD 3
+#endif
+constexpr int kAhead = CP25_M16_AHEAD;  // MFMA phase: operand pairs read ahead of their MFMAs
+#ifndef CP25_M16_SCHED
+#define CP25_M16_SCHED 1
+#endif
+constexpr bool kM16Sched = CP25_M16_SCHED;
+constexpr int kKBuf16 = kKBlk * kKStride16;        // 18432
+constexpr int kVBuf16 = kKBlk * kVStride16;        // 18432
+constexpr int kLds16 = 2 * kKBuf16 + 2 * kVBuf16;  // 73728
+
+__device__ __forceinline__ float group4_sum(float x) {  // sum over the 4 lane groups of 16 (lanes c, c+16, c+32, c+48)
+  x += __shfl_xor(x, 16);
+  return x + __shfl_xor(x, 32);
+}
+
+template <int kKind, bool kPre>
+__global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[kLds16];
+  constexpr int KB1 = kKBuf16, VB0 = 2 * kKBuf16;
+
+  const int nwg = gridDim.x;
+  const int tile = xcd_remap(blockIdx.x, nwg);
+  const int qb = tile % a.nqb;
+  const int bhs = tile / a.nqb;
+  const int split = bhs % a.nsplit, bh = bhs / a.nsplit;
+  const int b = bh / a.H, h = bh % a.H;
+  const int key0 = split * a.tps * kKBlk;
+  const int Lk = min(a.Lk - key0, a.tps * kKBlk);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int c16 = lane & 15;
+  const int g = lane >> 4;
+  const bool group_b = __builtin_amdgcn_readfirstlane(tid) >= kThreads / 2;
+
+  const unsigned short* qp = a.q + b * a.q_sb + h * a.q_sh;
+  const unsigned short* kp = a.k + b * a.k_sb + h * a.k_sh + (int64_t)key0 * a.k_sl;
+  const unsigned short* vp = a.v + b * a.v_sb + h * a.v_sh + (int64_t)key0 * a.v_sl;
+
+  // ---- Q fragments (B operand): Q[16 qh + c][32 s + 8 g .. +7] ----
+  int q_row[2];
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int qh = 0; qh < 2; ++qh) {
+    q_row[qh] = qb * kQBlk + wave * kQRows + 16 * qh + c16;
+    const unsigned short* src = qp + (int64_t)min(q_row[qh], a.Lq - 1) * a.q_sl + 8 * g;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[qh][s] = *reinterpret_cast<const bf16x8*>(src + 32 * s);
+  }
+
+  f32x4 o[8][2];
+#pragma unroll
+  for (int d = 0; d < 8; ++d)
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) o[d][qh] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float l_run[2] = {0.f, 0.f};
+  float m_run[2] = {0.f, 0.f};
+  if constexpr (!kPre) {  // bounded shift: m = max(|q_row| * kbound * scale_log2 - kTop, 0)
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      float qq = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = static_cast<float>(qf[qh][s][e]);
+          qq = fmaf(x, x, qq);
+        }
+      m_run[qh] = fmaxf(sqrtf(group4_sum(qq)) * a.kbound * a.scale_log2 - kTop, 0.f);
+    }
+  }
+
+  const int ntiles = (Lk + kKBlk - 1) / kKBlk;
+
+  // staging (as attn_fwd_d128): a group's 256 threads own rows u/16 + 16 i, chunk u%16 of a 64 x 128 tile
+  const int u = tid & (kThreads / 2 - 1);
+  const int srow = u >> 4, sch = u & 15;
+  const int64_t sl = group_b ? a.k_sl : a.v_sl;
+  const char* sbase = group_b ? (const char*)kp : (const char*)vp;
+  const int st_off = (int)(srow * sl * 2) + sch * 16, st_step = (int)(16 * sl * 2);
+  u32x4 st[4];
+  auto load_tile = [&](int t) __attribute__((always_inline)) {
+    const int rows = min(Lk - t * kKBlk, kKBlk);
+    const int nbytes = rows > 0 ? (int)((rows - 1) * sl * 2) + 2 * kD : 0;
+#ifdef CP25_LAB_TILE0  // lab only (wrong results): every tile re-reads key tile 0 (cache-resident K/V stream)
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)sbase, (short)0, nbytes, 0x00020000);
+#else
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(sbase + (int64_t)t * kKBlk * sl * 2), (short)0,
+                                                        nbytes, 0x00020000);
+#endif
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      st[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, st_off + i * st_step, 0, 0));
+  };
+  char* const k_wr = smem + srow * kKStride16 + sch * 16;
+  char* const v_wr = smem + VB0 + srow * kVStride16 + sch * 16;
+  auto write_k = [&](auto BUF) __attribute__((always_inline)) {
+    constexpr int kb = decltype(BUF)::value ? KB1 : 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(k_wr + kb + 16 * i * kKStride16) = st[i];
+  };
+  auto write_v = [&](auto BUF) __attribute__((always_inline)) {
+    constexpr int vb = decltype(BUF)::value ? kVBuf16 : 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(v_wr + vb + 16 * i * kVStride16) = st[i];
+  };
+
+  // per-lane LDS read bases; everything else is an immediate offset
+  const char* const k_rd = smem + c16 * kKStride16 + 16 * g;  // + KB + 16 kb rows + 64 s bytes
+  const char* const v_rd = smem + VB0 + (4 * g + (c16 >> 2)) * kVStride16 + 8 * (c16 & 3);  // + VB + rows + 32 db
+  const unsigned k_rd_lds = (unsigned)(uintptr_t)(lds_char_ptr)k_rd;
+  const unsigned v_rd_lds = (unsigned)(uintptr_t)(lds_char_ptr)v_rd;
+
+  const int ragged_tile = (Lk % kKBlk) != 0 ? Lk / kKBlk : -1;
+
+  f32x4 S[4][2];   // S^T of the tile awaiting its softmax: [key block][query half]
+  bf16x8 pb[2][2]; // P^T of the tile awaiting its P.V: [key step][query half]
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+
+  auto qk_mma = [&](auto BUF) __attribute__((always_inline)) {
+    constexpr int kb = decltype(BUF)::value ? KB1 : 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(k_rd + kb + k4 * 16 * kKStride16 + 64 * s);
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh)
+          S[k4][qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qh][s], s == 0 ? zero4 : S[k4][qh], 0, 0, 0);
+      }
+  };
+  auto softmax = [&](int t) __attribute__((always_inline)) {
+    if (__builtin_expect(t == ragged_tile, 0)) {
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = t * kKBlk + 16 * k4 + 4 * g + i;
+          if (key >= Lk) {
+            S[k4][0][i] = -INFINITY;
+            S[k4][1][i] = -INFINITY;
+          }
+        }
+    }
+    asm volatile("" : "+v"(S[0][0]), "+v"(S[0][1]), "+v"(S[1][0]), "+v"(S[1][1]), "+v"(S[2][0]), "+v"(S[2][1]),
+                 "+v"(S[3][0]), "+v"(S[3][1]));
+    // contract guard (as attn_fwd_d128): an overflowed row sum poisons the rows instead of a silent wrong answer
+    if (__builtin_expect(__any(fmaxf(l_run[0], l_run[1]) > 3.0e38f), 0)) {
+      const float nan = __uint_as_float(0x7fc00000u);
+#pragma unroll
+      for (int d = 0; d < 8; ++d) o[d][0] = o[d][1] = f32x4{nan, nan, nan, nan};
+    }
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      float psum = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float sv = S[2 * ks + (j >> 2)][qh][j & 3];
+          const float p = __builtin_amdgcn_exp2f(kPre ? sv : fmaf(sv, a.scale_log2, -m_run[qh]));
+          psum += p;
+          v[j] = static_cast<__bf16>(p);
+        }
+        pb[ks][qh] = v;
+      }
+      l_run[qh] += psum;
+    }
+    asm volatile("" ::"v"(pb[0][0]), "v"(pb[0][1]), "v"(pb[1][0]), "v"(pb[1][1]), "v"(l_run[0]), "v"(l_run[1]));
+  };
+
+  typedef std::integral_constant<int, 0> B0;
+  typedef std::integral_constant<int, 1> B1;
+
+  // ---- prologue: K(0), V(0) -> buffer 0; K(1) -> buffer 1; S(0) for everyone, P(0) for A ----
+  load_tile(0);
+  if (group_b) write_k(B0{}); else write_v(B0{});
+  if (group_b) {
+    load_tile(1);
+    write_k(B1{});
+    load_tile(2);  // written in phase 0
+  } else {
+    load_tile(1);  // written in phase 1
+  }
+  __syncthreads();
+  qk_mma(B0{});
+  if (!group_b) softmax(0);
+  __syncthreads();
+
+  // one MFMA phase: Q K^T of tile t+1 and P.V of tile t (64 MFMAs of 16 cycles = the 32 of the d128 kernel).
+  // Operand pair n (one fragment, two MFMAs, one per query half): n < 16 the K fragment (kb = n & 3, s = n >> 2),
+  // n >= 16 the V^T fragment (db = (n - 16) & 7, ks = (n - 16) >> 3). Reads are inline asm issued kAhead pairs
+  // ahead into a (kAhead + 1)-deep ring, each pair preceded by a counted lgkmcnt wait naming its operand.
+  auto mfma_phase = [&](auto PAR) __attribute__((always_inline)) {
+    constexpr int par = decltype(PAR)::value;
+    constexpr int kbuf = (par ^ 1) ? KB1 : 0;  // K(t+1)
+    constexpr int vbuf = par ? kVBuf16 : 0;    // V(t), relative to VB0
+    constexpr int kR = kAhead + 1;
+    bf16x8 ring[kR];
+    auto issue = [&](auto NC) __attribute__((always_inline)) {
+      constexpr int n = decltype(NC)::value;
+      if constexpr (n < 16) {
+        constexpr int off = kbuf + (n & 3) * 16 * kKStride16 + 64 * (n >> 2);
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ring[n % kR]) : "v"(k_rd_lds), "i"(off));
+      } else if constexpr (n < 32) {
+        constexpr int off = vbuf + 32 * ((n - 16) >> 3) * kVStride16 + 32 * ((n - 16) & 7);
+        s16x4 lo, hi;
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(v_rd_lds), "i"(off));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(v_rd_lds), "i"(off + 16 * kVStride16));
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        ring[n % kR] = __builtin_bit_cast(bf16x8, r);
+      }
+    };
+    constexpr auto nreads = [](int n) constexpr { return n < 16 ? 1 : (n < 32 ? 2 : 0); };
+    __builtin_amdgcn_s_setprio(1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    static_for<kAhead>(issue);
+    static_for<32>([&](auto NC) __attribute__((always_inline)) {
+      constexpr int n = decltype(NC)::value;
+      issue(std::integral_constant<int, n + kAhead>{});
+      constexpr int pending = [=]() constexpr {
+        int p = 0;
+        for (int i = 1; i <= kAhead; ++i) p += nreads(n + i);
+        return p;
+      }();
+      asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(ring[n % kR]) : "i"(pending));
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) {
+        if constexpr (n < 16) {
+          S[n & 3][qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[n % kR], qf[qh][n >> 2], n < 4 ? zero4 : S[n & 3][qh],
+                                                                  0, 0, 0);
+        } else {
+          o[(n - 16) & 7][qh] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[n % kR], pb[(n - 16) >> 3][qh], o[(n - 16) & 7][qh], 0, 0, 0);
+        }
+      }
+      // program order = issue order: read n + kAhead, wait, the pair's two MFMAs (the scheduler otherwise sinks
+      // MFMAs below later reads and renames accumulators, which costs v_mov copies)
+      if constexpr (kM16Sched) __builtin_amdgcn_sched_barrier(0);
+    });
+    __builtin_amdgcn_s_setprio(0);
+  };
+  if (!group_b) {
+    // group A: phase 2t MFMA, phase 2t+1 softmax(t+1) + V(t+1) staging
+    auto step = [&](auto PAR, int t) __attribute__((always_inline)) {
+      constexpr int par = decltype(PAR)::value;
+      mfma_phase(PAR);
+      ATTN_STAMP(t, 0);
+      __syncthreads();
+      ATTN_STAMP(t, 1);
+      if (t + 1 < ntiles) {
+        write_v(std::integral_constant<int, par ^ 1>{});
+        softmax(t + 1);
+        ATTN_STAMP(t, 5);
+        load_tile(t + 2);
+      }
+      ATTN_STAMP(t, 2);
+      __syncthreads();
+      ATTN_STAMP(t, 3);
+    };
+    for (int t = 0; t + 1 < ntiles; t += 2) {
+      step(B0{}, t);
+      step(B1{}, t + 1);
+    }
+    if (ntiles & 1) step(B0{}, ntiles - 1);
+  } else {
+    // group B: phase 2t softmax(t) + K(t+2) staging, phase 2t+1 MFMA
+    auto step = [&](auto PAR, int t) __attribute__((always_inline)) {
+      if (t + 2 < ntiles) write_k(PAR);
+      softmax(t);
+      ATTN_STAMP(t, 4);
+      if (t + 2 < ntiles) load_tile(t + 3);
+      ATTN_STAMP(t, 0);
+      __syncthreads();
+      ATTN_STAMP(t, 1);
+      mfma_phase(PAR);
+      ATTN_STAMP(t, 2);
+      __syncthreads();
+      ATTN_STAMP(t, 3);
+    };
+    for (int t = 0; t + 1 < ntiles; t += 2) {
+      step(B0{}, t);
+      step(B1{}, t + 1);
+    }
+    if (ntiles & 1) step(B0{}, ntiles - 1);
+  }
+
+  // ---- epilogue: lane holds O^T[16 db + 4 g + i][16 qh + c]: row q_row[qh], d = 16 db + 4 g + (0..3) ----
+#pragma unroll
+  for (int qh = 0; qh < 2; ++qh) {
+    const float l_tot = group4_sum(l_run[qh]);
+    const float inv = 1.f / l_tot;
+    if (q_row[qh] >= a.Lq) continue;
+    if (a.nsplit > 1) {
+      const int64_t row = ((int64_t)(split * a.B + b) * a.H + h) * a.Lq + q_row[qh];
+      float* op = a.o_part + row * kD + 4 * g;
+#pragma unroll
+      for (int db = 0; db < 8; ++db) {
+        f32x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = o[db][qh][e] * inv;
+        *reinterpret_cast<f32x4*>(op + 16 * db) = w;
+      }
+      if (g == 0) a.lse_part[row] = m_run[qh] + __log2f(l_tot);
+    } else {
+      unsigned short* op = a.o + b * a.o_sb + h * a.o_sh + (int64_t)q_row[qh] * a.o_sl + 4 * g;
+#pragma unroll
+      for (int db = 0; db < 8; ++db) {
+        u16x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = f2bf(o[db][qh][e] * inv);
+        *reinterpret_cast<u16x4*>(op + 16 * db) = w;
+      }
+    }
+  }
+}
+
 int g_num_cus = 0;
+
+// CP25_ATTN_MFMA=16: the bounded / prescaled bf16 forms on attn_fwd_m16 (16x16x32) instead of attn_fwd_d128;
+// read per launch (A/B runs switch it in-process)
+bool attn_m16() {
+  const char* e = getenv("CP25_ATTN_MFMA");
+  return e && e[0] == '1';
+}
 
 // which bounded/prescaled kernel runs: attn_fwd_d128 (two waves per SIMD, ping-pong; the default) or,
 // with CP25_ATTN_KERNEL=1w, attn_fwd_1w (one wave per SIMD). Measured at the metric shape, prescaled
@@ -1322,6 +1675,10 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
     if (bhn * a.nchunk > 0x7fffffff) return CP25_ERR_INVAL;
     hipLaunchKernelGGL((attn_fwd_d128<1, true, true, false, true>), dim3((unsigned)(bhn * a.nchunk)), dim3(kThreads), 0,
                        stream, a);
+  } else if ((prescaled || fixed) && attn_m16()) {
+    auto kernel = prescaled ? (Lk <= 4096 ? attn_fwd_m16<1, true> : attn_fwd_m16<0, true>)
+                            : (Lk <= 4096 ? attn_fwd_m16<1, false> : attn_fwd_m16<0, false>);
+    hipLaunchKernelGGL(kernel, dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
   } else {
     auto kernel = prescaled ? (Lk <= 4096 ? attn_fwd_d128<1, true, true> : attn_fwd_d128<0, true, true>)
                   : Lk <= 4096 ? (fixed ? attn_fwd_d128<1, true> : attn_fwd_d128<1, false>)

@@ -11,7 +11,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ("attn_fwd_d128<0", "attn_fwd_1w<0")  # self-attention instantiations (d128 <0, true>: bounded shift)
+KERNELS = ("attn_fwd_d128<0", "attn_fwd_1w<0", "attn_fwd_m16<0")  # self-attention instantiations (d128 <0, true>: bounded shift)
 FLOP = 4.0 * 2 * 16 * 109120 * 109120 * 128
 ALGO_BYTES = 4 * 2 * 16 * 109120 * 128 * 2  # Q, K, V read once, O written once (bf16)
 
