@@ -1191,6 +1191,10 @@ constexpr int kAhead = CP25_M16_AHEAD;  // MFMA phase: operand pairs read ahead 
 #define CP25_M16_SCHED 1
 #endif
 constexpr bool kM16Sched = CP25_M16_SCHED;
+#ifndef CP25_M16_EARLY_LOAD
+#define CP25_M16_EARLY_LOAD 0
+#endif
+constexpr bool kEarlyLoad = CP25_M16_EARLY_LOAD;  // K/V staging loads issued before the softmax instead of after
 constexpr int kKBuf16 = kKBlk * kKStride16;        // 18432
 constexpr int kVBuf16 = kKBlk * kVStride16;        // 18432
 constexpr int kLds16 = 2 * kKBuf16 + 2 * kVBuf16;  // 73728
@@ -1440,9 +1444,10 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
       ATTN_STAMP(t, 1);
       if (t + 1 < ntiles) {
         write_v(std::integral_constant<int, par ^ 1>{});
+        if constexpr (kEarlyLoad) load_tile(t + 2);  // the staging registers are free once written to LDS
         softmax(t + 1);
         ATTN_STAMP(t, 5);
-        load_tile(t + 2);
+        if constexpr (!kEarlyLoad) load_tile(t + 2);
       }
       ATTN_STAMP(t, 2);
       __syncthreads();
@@ -1457,9 +1462,10 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
     // group B: phase 2t softmax(t) + K(t+2) staging, phase 2t+1 MFMA
     auto step = [&](auto PAR, int t) __attribute__((always_inline)) {
       if (t + 2 < ntiles) write_k(PAR);
+      if (kEarlyLoad && t + 2 < ntiles) load_tile(t + 3);
       softmax(t);
       ATTN_STAMP(t, 4);
-      if (t + 2 < ntiles) load_tile(t + 3);
+      if (!kEarlyLoad && t + 2 < ntiles) load_tile(t + 3);
       ATTN_STAMP(t, 0);
       __syncthreads();
       ATTN_STAMP(t, 1);
