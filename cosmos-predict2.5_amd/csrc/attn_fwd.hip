@@ -1195,6 +1195,19 @@ constexpr bool kM16Sched = CP25_M16_SCHED;
 #define CP25_M16_EARLY_LOAD 0
 #endif
 constexpr bool kEarlyLoad = CP25_M16_EARLY_LOAD;  // K/V staging loads issued before the softmax instead of after
+#ifndef CP25_M16_LSUM
+#define CP25_M16_LSUM 1
+#endif
+// row sums by MFMA: lsum[qh] += ones^T P^T (one 16x16x32 MFMA per key step and query half, 4 per tile) instead of
+// 32 v_add_f32 per tile in the softmax phase; the sum is then of the bf16 P the P.V MFMAs used, and it arrives
+// complete in every lane (the MFMA reduces over the 4 lane groups)
+constexpr bool kLsum = CP25_M16_LSUM;
+#ifndef CP25_M16_PV_FIRST
+#define CP25_M16_PV_FIRST 1
+#endif
+// MFMA phase order: P.V(t) before Q K^T(t+1), so P^T (16 VGPRs) is dead before S^T (32) is written and the two
+// share registers (the other order keeps both live through the phase)
+constexpr bool kPvFirst = CP25_M16_PV_FIRST;
 constexpr int kKBuf16 = kKBlk * kKStride16;        // 18432
 constexpr int kVBuf16 = kKBlk * kVStride16;        // 18432
 constexpr int kLds16 = 2 * kKBuf16 + 2 * kVBuf16;  // 73728
@@ -1246,6 +1259,9 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
 #pragma unroll
     for (int qh = 0; qh < 2; ++qh) o[d][qh] = f32x4{0.f, 0.f, 0.f, 0.f};
   float l_run[2] = {0.f, 0.f};
+  f32x4 lsum[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  typedef short s16x8v __attribute__((ext_vector_type(8)));
+  const bf16x8 ones8 = __builtin_bit_cast(bf16x8, s16x8v{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80});
   float m_run[2] = {0.f, 0.f};
   if constexpr (!kPre) {  // bounded shift: m = max(|q_row| * kbound * scale_log2 - kTop, 0)
 #pragma unroll
@@ -1337,7 +1353,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
     asm volatile("" : "+v"(S[0][0]), "+v"(S[0][1]), "+v"(S[1][0]), "+v"(S[1][1]), "+v"(S[2][0]), "+v"(S[2][1]),
                  "+v"(S[3][0]), "+v"(S[3][1]));
     // contract guard (as attn_fwd_d128): an overflowed row sum poisons the rows instead of a silent wrong answer
-    if (__builtin_expect(__any(fmaxf(l_run[0], l_run[1]) > 3.0e38f), 0)) {
+    if (__builtin_expect(__any(kLsum ? fmaxf(lsum[0][0], lsum[1][0]) > 3.0e38f : fmaxf(l_run[0], l_run[1]) > 3.0e38f), 0)) {
       const float nan = __uint_as_float(0x7fc00000u);
 #pragma unroll
       for (int d = 0; d < 8; ++d) o[d][0] = o[d][1] = f32x4{nan, nan, nan, nan};
@@ -1352,12 +1368,12 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
         for (int j = 0; j < 8; ++j) {
           const float sv = S[2 * ks + (j >> 2)][qh][j & 3];
           const float p = __builtin_amdgcn_exp2f(kPre ? sv : fmaf(sv, a.scale_log2, -m_run[qh]));
-          psum += p;
+          if constexpr (!kLsum) psum += p;
           v[j] = static_cast<__bf16>(p);
         }
         pb[ks][qh] = v;
       }
-      l_run[qh] += psum;
+      if constexpr (!kLsum) l_run[qh] += psum;
     }
     asm volatile("" ::"v"(pb[0][0]), "v"(pb[0][1]), "v"(pb[1][0]), "v"(pb[1][1]), "v"(l_run[0]), "v"(l_run[1]));
   };
@@ -1392,11 +1408,13 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
     bf16x8 ring[kR];
     auto issue = [&](auto NC) __attribute__((always_inline)) {
       constexpr int n = decltype(NC)::value;
-      if constexpr (n < 16) {
-        constexpr int off = kbuf + (n & 3) * 16 * kKStride16 + 64 * (n >> 2);
+      if constexpr (kPvFirst ? (n >= 16 && n < 32) : n < 16) {
+        constexpr int m = kPvFirst ? n - 16 : n;
+        constexpr int off = kbuf + (m & 3) * 16 * kKStride16 + 64 * (m >> 2);
         asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ring[n % kR]) : "v"(k_rd_lds), "i"(off));
       } else if constexpr (n < 32) {
-        constexpr int off = vbuf + 32 * ((n - 16) >> 3) * kVStride16 + 32 * ((n - 16) & 7);
+        constexpr int m = kPvFirst ? n : n - 16;
+        constexpr int off = vbuf + 32 * (m >> 3) * kVStride16 + 32 * (m & 7);
         s16x4 lo, hi;
         asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(v_rd_lds), "i"(off));
         asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(v_rd_lds), "i"(off + 16 * kVStride16));
@@ -1405,7 +1423,9 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
         ring[n % kR] = __builtin_bit_cast(bf16x8, r);
       }
     };
-    constexpr auto nreads = [](int n) constexpr { return n < 16 ? 1 : (n < 32 ? 2 : 0); };
+    constexpr auto nreads = [](int n) constexpr {
+      return n >= 32 ? 0 : ((kPvFirst ? n >= 16 : n < 16) ? 1 : 2);
+    };
     __builtin_amdgcn_s_setprio(1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     static_for<kAhead>(issue);
@@ -1420,18 +1440,31 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
       asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(ring[n % kR]) : "i"(pending));
 #pragma unroll
       for (int qh = 0; qh < 2; ++qh) {
-        if constexpr (n < 16) {
-          S[n & 3][qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[n % kR], qf[qh][n >> 2], n < 4 ? zero4 : S[n & 3][qh],
+        if constexpr (kPvFirst ? n >= 16 : n < 16) {
+          constexpr int m = kPvFirst ? n - 16 : n;
+          S[m & 3][qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[n % kR], qf[qh][m >> 2], m < 4 ? zero4 : S[m & 3][qh],
                                                                   0, 0, 0);
         } else {
-          o[(n - 16) & 7][qh] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[n % kR], pb[(n - 16) >> 3][qh], o[(n - 16) & 7][qh], 0, 0, 0);
+          constexpr int m = kPvFirst ? n : n - 16;
+          o[m & 7][qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[n % kR], pb[m >> 3][qh], o[m & 7][qh], 0, 0, 0);
         }
       }
       // program order = issue order: read n + kAhead, wait, the pair's two MFMAs (the scheduler otherwise sinks
       // MFMAs below later reads and renames accumulators, which costs v_mov copies)
+      if constexpr (kLsum && kPvFirst && n == 15) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int qh = 0; qh < 2; ++qh) lsum[qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones8, pb[ks][qh], lsum[qh], 0, 0, 0);
+      }
       if constexpr (kM16Sched) __builtin_amdgcn_sched_barrier(0);
     });
+    if constexpr (kLsum && !kPvFirst) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) lsum[qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones8, pb[ks][qh], lsum[qh], 0, 0, 0);
+    }
     __builtin_amdgcn_s_setprio(0);
   };
   if (!group_b) {
@@ -1484,7 +1517,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
   // ---- epilogue: lane holds O^T[16 db + 4 g + i][16 qh + c]: row q_row[qh], d = 16 db + 4 g + (0..3) ----
 #pragma unroll
   for (int qh = 0; qh < 2; ++qh) {
-    const float l_tot = group4_sum(l_run[qh]);
+    const float l_tot = kLsum ? lsum[qh][0] : group4_sum(l_run[qh]);
     const float inv = 1.f / l_tot;
     if (q_row[qh] >= a.Lq) continue;
     if (a.nsplit > 1) {
@@ -1513,11 +1546,12 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
 
 int g_num_cus = 0;
 
-// CP25_ATTN_MFMA=16: the bounded / prescaled bf16 forms on attn_fwd_m16 (16x16x32) instead of attn_fwd_d128;
-// read per launch (A/B runs switch it in-process)
+// the bounded / prescaled bf16 forms run on attn_fwd_m16 (16x16x32); CP25_ATTN_MFMA=32 selects attn_fwd_d128
+// (32x32x16) instead. Same box, metric shape, prescaled: 143.3 / 143.6 ms vs 149.6 / 149.3 ms per launch
+// (profiles/r2/attn_m16/). Read per launch (A/B runs and tests switch it in-process)
 bool attn_m16() {
   const char* e = getenv("CP25_ATTN_MFMA");
-  return e && e[0] == '1';
+  return !(e && e[0] == '3');
 }
 
 // which bounded/prescaled kernel runs: attn_fwd_d128 (two waves per SIMD, ping-pong; the default) or,

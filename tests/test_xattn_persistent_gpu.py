@@ -1,7 +1,9 @@
 """Persistent short-KV attention (cp25_attn_fwd_prescaled at Lk <= 1024: the DiT's text cross-attention,
 minimal_v4_dit.py:1216-1226, attention.py:90-181): one workgroup per CU runs a run of query blocks of one (b, h)
 as a single key-tile stream (opt-in, CP25_XATTN_KERNEL=persist, read per launch). Same per-block arithmetic as
-the one-workgroup-per-block kernel (the default), so the two are compared bit for bit, and both against fp32 math.
+the one-workgroup-per-block 32x32x16 kernel (attn_fwd_d128, CP25_ATTN_MFMA=32; the default per-block kernel is
+the 16x16x32 attn_fwd_m16, tests/test_attn_m16_gpu.py), so the two are compared bit for bit, and both against
+fp32 math.
 Covers ragged key tiles, one-tile blocks (Lk <= 64), ragged query blocks, chunks of one block, and strided
 token-major views as the DiT passes them."""
 import os
@@ -21,13 +23,21 @@ def _normed(shape, g, device):
     return (t * torch.rsqrt(t.pow(2).mean(-1, keepdim=True) + 1e-6)).to(device, torch.bfloat16)
 
 
+def _select(blocks):
+    os.environ["CP25_XATTN_KERNEL" if not blocks else "CP25_ATTN_MFMA"] = "persist" if not blocks else "32"
+
+
+def _unselect():
+    os.environ.pop("CP25_XATTN_KERNEL", None)
+    os.environ.pop("CP25_ATTN_MFMA", None)
+
+
 def _run(q, k, v, nb, blocks):
-    if not blocks:
-        os.environ["CP25_XATTN_KERNEL"] = "persist"
+    _select(blocks)
     try:
         return N.attn_fwd(q, k, v, norm_bounds=nb, prescaled=True, n_split=1)
     finally:
-        os.environ.pop("CP25_XATTN_KERNEL", None)
+        _unselect()
 
 
 @pytest.mark.parametrize("B,H,Lq,Lk", [(2, 16, 20000, 512), (1, 2, 777, 300), (1, 3, 5000, 64), (2, 4, 3333, 1000),
@@ -61,13 +71,12 @@ def test_xattn_persistent_strided_views(device):
     outs = []
     for blocks in (False, True):
         o = torch.full((n, B, H * 128), float("nan"), device=device, dtype=torch.bfloat16)
-        if not blocks:
-            os.environ["CP25_XATTN_KERNEL"] = "persist"
+        _select(blocks)
         try:
             N.attn_fwd(q.transpose(0, 1), k, v, out=o.view(n, B, H, 128).transpose(0, 1), norm_bounds=nb,
                        prescaled=True)
         finally:
-            os.environ.pop("CP25_XATTN_KERNEL", None)
+            _unselect()
         outs.append(o)
     assert torch.isfinite(outs[0].float()).all()
     assert torch.equal(outs[0], outs[1])

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--H", type=int, default=16)
     ap.add_argument("--t0", type=int, default=200)
     ap.add_argument("--bounded", action="store_true", help="RMS-normed q/k + cp25_attn_fwd_bounded (the DiT's form)")
+    ap.add_argument("--prescaled", action="store_true", help="RMS-normed k, q * scale * log2(e) + cp25_attn_fwd_prescaled")
     ap.add_argument("--lib", default=os.path.join(ROOT, "tools", "lab", "libattn_probe.so"))
     a = ap.parse_args()
     lib = ctypes.CDLL(a.lib)
@@ -33,13 +34,19 @@ def main():
     lib.cp25_attn_fwd_bounded.argtypes = [P, P, P, P] + [ctypes.c_int] * 5 + [P] * 4 + [ctypes.c_float] * 3 + \
         [ctypes.c_int, P, ctypes.c_size_t, P]
     lib.cp25_attn_fwd_bounded.restype = ctypes.c_int
+    lib.cp25_attn_fwd_prescaled.argtypes = [P, P, P, P] + [ctypes.c_int] * 5 + [P] * 4 + [ctypes.c_float] * 2 + \
+        [ctypes.c_int, P, ctypes.c_size_t, P]
+    lib.cp25_attn_fwd_prescaled.restype = ctypes.c_int
     lib.cp25_attn_probe_set.argtypes = [P, ctypes.c_int]
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     q, k, v = (torch.randn(a.B, a.L, a.H, 128, device=dev, generator=g).to(torch.bfloat16) for _ in range(3))
-    if a.bounded:
+    if a.bounded or a.prescaled:
         for t in (q, k):
             t.copy_((t.float() * torch.rsqrt(t.float().pow(2).mean(-1, keepdim=True) + 1e-6)).to(torch.bfloat16))
+    c = 128 ** -0.5 * 1.4426950408889634
+    if a.prescaled:
+        q.copy_((q.float() * c).to(torch.bfloat16))
     o = torch.empty_like(q)
     probe = torch.zeros(8 * 8 * 32 * 8, dtype=torch.int64, device=dev)
 
@@ -50,7 +57,11 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
 
     def run():
-        if a.bounded:
+        if a.prescaled:
+            nb = 128 ** 0.5 * 1.02
+            rc = lib.cp25_attn_fwd_prescaled(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), a.B, a.H, a.L, a.L,
+                                             128, *[ctypes.cast(s, P) for s in st], nb * c, nb, 1, None, 0, stream)
+        elif a.bounded:
             nb = 128 ** 0.5 * 1.02
             rc = lib.cp25_attn_fwd_bounded(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), a.B, a.H, a.L, a.L,
                                            128, *[ctypes.cast(s, P) for s in st], 128 ** -0.5, nb, nb, 1, None, 0,

@@ -1,0 +1,20 @@
+# m16 (P.V first) variants: phase anatomy (prescaled) + metric-shape A/B vs d128
+set -o pipefail
+export PYTHONUNBUFFERED=1
+mkdir -p gpurun_out/m16d
+rm -f gpurun_out/m16d/*.log
+CP25_ATTN_MFMA=32 timeout -k 10 120 python tools/attn_probe.py --L 109120 --prescaled --t0 600 --lib tools/lab/libattn_probe_base.so >> gpurun_out/m16d/probe.log 2>&1 || exit 1
+for n in base ahead2 lsum; do
+  CP25_ATTN_MFMA=16 timeout -k 10 120 python tools/attn_probe.py --L 109120 --prescaled --t0 600 --lib tools/lab/libattn_probe_$n.so >> gpurun_out/m16d/probe.log 2>&1 || exit 1
+done
+grep '^{' gpurun_out/m16d/probe.log | python3 -c "
+import json,sys
+for l in sys.stdin:
+    d=json.loads(l); print(round(d['ms'],1), 'A', d['A'], 'B', d['B'])"
+for i in 1 2; do
+  CP25_ATTN_MFMA=32 timeout -k 10 120 python tools/bench_attn.py --fused --bounded --prescaled --iters 4 >> gpurun_out/m16d/ab.log 2>&1 || exit 1
+  for n in base ahead2 lsum; do
+    CP25_ATTN_MFMA=16 timeout -k 10 120 python tools/bench_attn.py --fused --bounded --prescaled --iters 4 --lib tools/lab/libcp25_$n.so >> gpurun_out/m16d/ab.log 2>&1 || exit 1
+  done
+done
+grep -o '"lib": "[^"]*"\|"ms": [0-9.]*\|"check_rel_l2": [0-9.e-]*' gpurun_out/m16d/ab.log | paste - - -
