@@ -16,6 +16,7 @@ re-designed for the sampler hot path:
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
@@ -211,6 +212,8 @@ class MinimalV1LVGDiT:
         self.attention_precision = "bf16"
         # the CFG pair's shared block-0 prefix runs once (see _blocks); False: every entry computes it
         self.share_cfg_block0 = True
+        # MLP layer1 + GELU: "own" = cp25_gemm_epi with the GELU epilogue, "lib" = hipBLASLt + cp25_gelu
+        self.mlp1_gemm = os.environ.get("CP25_MLP1_GEMM", "own")
 
     def set_linear_precision(self, precision: str) -> None:
         """"bf16" (default, the reference's arithmetic) or "fp8": the 28 blocks' q/k/v, output, cross-q,
@@ -279,6 +282,12 @@ class MinimalV1LVGDiT:
             ent = (w8, sc.t().contiguous())  # [N, K] fp8, [1, N] fp32
             self._fp8_w[key] = ent
         return ent
+
+    def _mlp1_fused(self, x, w: torch.Tensor) -> bool:
+        """GPT2FeedForward layer1 + GELU (minimal_v4_dit.py:249-254) on cp25_gemm_epi's GELU epilogue: bf16 linears,
+        shapes the kernel is built for, and `mlp1_gemm == "own"` (CP25_MLP1_GEMM=lib keeps hipBLASLt + cp25_gelu)."""
+        return (self.mlp1_gemm == "own" and not isinstance(x, tuple) and self.linear_precision == "bf16"
+                and N.gemm_supported(w.shape[0], w.shape[1]))
 
     def _linear(self, x, w: torch.Tensor, key: str, gelu_in: bool = False) -> torch.Tensor:
         """y = x w^T for a block projection (x [M, K] bf16 contiguous, or an fp8 operand pair (q, scale)
@@ -654,8 +663,16 @@ class MinimalV1LVGDiT:
             h = N.ln_mod(x, sh, sc, x_st=Bs * D, x_sb=0 if Bs == 1 else D, y=y, gate=g_ca, x_out=x_new, **lnk)
             x = x_new
             # ---- MLP
-            u = self._linear(_rows(h, n * B), p[pre + "mlp.layer1.weight"], pre + "mlp.layer1")
-            y = self._linear(u, p[pre + "mlp.layer2.weight"], pre + "mlp.layer2", gelu_in=True)
+            h1 = _rows(h, n * B)
+            w1 = p[pre + "mlp.layer1.weight"]
+            if self._mlp1_fused(h1, w1):
+                # layer1 + exact-erf GELU in one hand-written MFMA GEMM (the epilogue applies it to the bf16
+                # product, as cp25_gelu would): the [n B, 4 D] hidden makes one HBM trip instead of three
+                u = N.gemm_epi(h1, w1, epilogue=N.EPI_GELU)
+                y = self._linear(u, p[pre + "mlp.layer2.weight"], pre + "mlp.layer2")
+            else:
+                u = self._linear(h1, w1, pre + "mlp.layer1")
+                y = self._linear(u, p[pre + "mlp.layer2.weight"], pre + "mlp.layer2", gelu_in=True)
             del u
             _, _, gate_prev = mod(i, 2)
             if i + 1 < cfg.num_blocks:

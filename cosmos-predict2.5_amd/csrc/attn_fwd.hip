@@ -1208,6 +1208,10 @@ constexpr bool kLsum = CP25_M16_LSUM;
 // MFMA phase order: P.V(t) before Q K^T(t+1), so P^T (16 VGPRs) is dead before S^T (32) is written and the two
 // share registers (the other order keeps both live through the phase)
 constexpr bool kPvFirst = CP25_M16_PV_FIRST;
+#ifndef CP25_M16_LSUM_FIRST
+#define CP25_M16_LSUM_FIRST 0
+#endif
+constexpr bool kLsumFirst = CP25_M16_LSUM_FIRST;  // row-sum MFMAs at the MFMA phase's start (else after the P.V pairs)
 constexpr int kKBuf16 = kKBlk * kKStride16;        // 18432
 constexpr int kVBuf16 = kKBlk * kVStride16;        // 18432
 constexpr int kLds16 = 2 * kKBuf16 + 2 * kVBuf16;  // 73728
@@ -1367,7 +1371,11 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float sv = S[2 * ks + (j >> 2)][qh][j & 3];
+#ifdef CP25_LAB_NOEXP  // lab only (wrong results): no transcendental in the softmax phase
+          const float p = sv;
+#else
           const float p = __builtin_amdgcn_exp2f(kPre ? sv : fmaf(sv, a.scale_log2, -m_run[qh]));
+#endif
           if constexpr (!kLsum) psum += p;
           v[j] = static_cast<__bf16>(p);
         }
@@ -1406,8 +1414,16 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
     constexpr int vbuf = par ? kVBuf16 : 0;    // V(t), relative to VB0
     constexpr int kR = kAhead + 1;
     bf16x8 ring[kR];
+#ifdef CP25_LAB_NOLDS
+#pragma unroll
+    for (int i = 0; i < kR; ++i) ring[i] = qf[1][i & 3];
+#endif
     auto issue = [&](auto NC) __attribute__((always_inline)) {
       constexpr int n = decltype(NC)::value;
+#ifdef CP25_LAB_NOLDS  // lab only (wrong results): the MFMA phase reads no LDS (operands stay in the ring)
+      if constexpr (true) {
+      } else
+#endif
       if constexpr (kPvFirst ? (n >= 16 && n < 32) : n < 16) {
         constexpr int m = kPvFirst ? n - 16 : n;
         constexpr int off = kbuf + (m & 3) * 16 * kKStride16 + 64 * (m >> 2);
@@ -1424,11 +1440,22 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
       }
     };
     constexpr auto nreads = [](int n) constexpr {
+#ifdef CP25_LAB_NOLDS
+      return 0 * n;
+#endif
       return n >= 32 ? 0 : ((kPvFirst ? n >= 16 : n < 16) ? 1 : 2);
     };
     __builtin_amdgcn_s_setprio(1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     static_for<kAhead>(issue);
+    if constexpr (kLsum && kLsumFirst) {
+      // the row-sum MFMAs need no LDS operand: they cover the first reads' latency at the phase start
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) lsum[qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones8, pb[ks][qh], lsum[qh], 0, 0, 0);
+      if constexpr (kM16Sched) __builtin_amdgcn_sched_barrier(0);
+    }
     static_for<32>([&](auto NC) __attribute__((always_inline)) {
       constexpr int n = decltype(NC)::value;
       issue(std::integral_constant<int, n + kAhead>{});
@@ -1451,7 +1478,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
       }
       // program order = issue order: read n + kAhead, wait, the pair's two MFMAs (the scheduler otherwise sinks
       // MFMAs below later reads and renames accumulators, which costs v_mov copies)
-      if constexpr (kLsum && kPvFirst && n == 15) {
+      if constexpr (kLsum && !kLsumFirst && kPvFirst && n == 15) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -1459,7 +1486,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
       }
       if constexpr (kM16Sched) __builtin_amdgcn_sched_barrier(0);
     });
-    if constexpr (kLsum && !kPvFirst) {
+    if constexpr (kLsum && !kLsumFirst && !kPvFirst) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll

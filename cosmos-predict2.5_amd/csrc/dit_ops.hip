@@ -258,7 +258,7 @@ __global__ void __launch_bounds__(256) gelu_kernel(unsigned short* __restrict__ 
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const float a = bf2f(w[e]);
-    o[e] = f2bf(0.5f * a * (1.f + erff(a * 0.70710678118654752440f)));
+    o[e] = f2bf(gelu_erf(a));
   }
   *reinterpret_cast<u16x8*>(x + i * 8) = o;
 }

@@ -48,9 +48,7 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, lds_void_ptr 
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dst, 16, voffset, soffset, 0, 0);
 }
 
-__device__ __forceinline__ float gelu_exact(float a) {
-  return 0.5f * a * (1.f + erff(a * 0.70710678118654752440f));  // = cp25_gelu
-}
+__device__ __forceinline__ float gelu_exact(float a) { return gelu_erf(a); }  // = cp25_gelu (cp25_common.h)
 
 template <int kEpi>
 __global__ void __launch_bounds__(kThreads, 1)

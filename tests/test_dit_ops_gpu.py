@@ -101,23 +101,41 @@ def test_head_rmsnorm_rope(device):
     assert torch.equal(buf[:, :D], ref_in[:, :D]) and torch.equal(buf[:, 2 * D:], ref_in[:, 2 * D:])
 
 
+def _gelu_exact_bf16(x):
+    """float64 x * Phi(x) with Phi = erfc(-x / sqrt 2) / 2 (no 1 + erf cancellation), rounded once to bf16."""
+    xd = x.double().cpu()
+    return (xd * 0.5 * torch.special.erfc(-xd * 0.5 ** 0.5)).to(torch.bfloat16)
+
+
+def _check_gelu(x, y):
+    """cp25_gelu (cp25_common.h gelu_erf) vs the correctly rounded GELU: within one bf16 ulp everywhere, equal on
+    >= 99.9 % of inputs. Outputs below the fp32 normal range may flush to zero on the GPU. torch's own GELU
+    (x/2 (1 + erf(x / sqrt 2)), what the reference's nn.GELU runs) cancels for x << 0: it is compared only on
+    x >= -2, where it is accurate."""
+    ref = _gelu_exact_bf16(x).to(y.device)
+    keep = ref.float().abs() >= 2.0 ** -126
+    ok, eq = bf16_ulp_close(y[keep], ref[keep])
+    assert ok, eq
+    assert (y[~keep].float().abs() <= 2.0 ** -126).all()
+    mild = x >= -2
+    ok_t, eq_t = bf16_ulp_close(y[mild], F.gelu(x[mild]))
+    assert ok_t, eq_t
+
+
 def test_gelu(device):
     x = (torch.randn(4096 * 3) * 3).to(device, torch.bfloat16)
-    ref = F.gelu(x)
-    N.gelu_(x)
-    ok, eq = bf16_ulp_close(x, ref)
-    assert ok, eq
+    y = x.clone()
+    N.gelu_(y)
+    _check_gelu(x, y)
 
 
 def test_gelu_every_bf16_value(device):
-    """Exact-erf GELU over every finite bf16 input (65 024 values), against torch's fp32 evaluation."""
+    """Exact-erf GELU over every finite bf16 input (65 024 values)."""
     bits = torch.arange(0, 1 << 16, dtype=torch.int32).to(torch.int16).view(torch.bfloat16)
     x = bits[torch.isfinite(bits.float())].to(device)
-    ref = F.gelu(x)
     y = x.clone()
     N.gelu_(y)
-    ok, eq = bf16_ulp_close(y, ref)
-    assert ok, eq
+    _check_gelu(x, y)
 
 
 def test_patchify_and_cfg_exact(device):
