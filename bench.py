@@ -36,7 +36,10 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "frames/sec, Predict2.5-2B Image2World 720p×121f, 35 UniPC steps, CP=1/8"
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 MFMA
 PRACTICAL_BF16_TFLOPS = 1499.4  # measured: hipBLASLt bf16 16384^3, random data (profiles/r2/peak/peak_gemm.log)
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r2", "attn_pmc", "SUMMARY.json")
+# measured: register-only v_mfma_f32_16x16x32_bf16 loop on random data, no memory traffic at all (the shape the
+# self-attention kernel runs; tools/lab/mfma_power.hip, profiles/r2/attn_m16/mfma_power_16x16x32.log)
+MFMA_LOOP_BF16_TFLOPS = 1880.3
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r2", "attn_pmc_m16", "SUMMARY.json")
 
 
 def parse():
@@ -241,7 +244,7 @@ def main():
             },
             "roofline": {
                 "bound": "mfma",
-                "kernel": {"bf16": "cp25_attn_fwd (DiT self-attention, bf16 MFMA)",
+                "kernel": {"bf16": "cp25_attn_fwd_prescaled (DiT self-attention, bf16 16x16x32 MFMA, attn_fwd_m16)",
                            "fp8qk": "cp25_attn_fwd_prescaled_fp8qk (DiT self-attention, fp8 Q K^T + bf16 P V MFMA)",
                            "fp8": "cp25_attn_fwd_prescaled_fp8 (DiT self-attention, fp8 Q K^T and P V MFMA)"}[
                                a.attention_precision],
@@ -254,6 +257,8 @@ def main():
                 # 2.4 GHz spec figure, is what a bf16 kernel can reach (profiles/r2/peak/peak_gemm.log)
                 "practical_peak": PRACTICAL_BF16_TFLOPS,
                 "frac_of_practical": achieved / PRACTICAL_BF16_TFLOPS,
+                "mfma_loop_peak": MFMA_LOOP_BF16_TFLOPS,
+                "frac_of_mfma_loop": achieved / MFMA_LOOP_BF16_TFLOPS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "launches_timed": len(attn_ms),

@@ -212,8 +212,9 @@ class MinimalV1LVGDiT:
         self.attention_precision = "bf16"
         # the CFG pair's shared block-0 prefix runs once (see _blocks); False: every entry computes it
         self.share_cfg_block0 = True
-        # MLP layer1 + GELU: "own" = cp25_gemm_epi with the GELU epilogue, "lib" = hipBLASLt + cp25_gelu
-        self.mlp1_gemm = os.environ.get("CP25_MLP1_GEMM", "own")
+        # MLP layer1 + GELU: "lib" (default) = hipBLASLt + cp25_gelu, "own" = cp25_gemm_epi with the GELU epilogue
+        # (measured 0.25 % slower end to end: 0.7264 vs 0.7282 frames/s, profiles/r2/gemm_gelu/)
+        self.mlp1_gemm = os.environ.get("CP25_MLP1_GEMM", "lib")
 
     def set_linear_precision(self, precision: str) -> None:
         """"bf16" (default, the reference's arithmetic) or "fp8": the 28 blocks' q/k/v, output, cross-q,
@@ -285,7 +286,7 @@ class MinimalV1LVGDiT:
 
     def _mlp1_fused(self, x, w: torch.Tensor) -> bool:
         """GPT2FeedForward layer1 + GELU (minimal_v4_dit.py:249-254) on cp25_gemm_epi's GELU epilogue: bf16 linears,
-        shapes the kernel is built for, and `mlp1_gemm == "own"` (CP25_MLP1_GEMM=lib keeps hipBLASLt + cp25_gelu)."""
+        shapes the kernel is built for, and `mlp1_gemm == "own"` (CP25_MLP1_GEMM=own; the default "lib" keeps hipBLASLt + cp25_gelu)."""
         return (self.mlp1_gemm == "own" and not isinstance(x, tuple) and self.linear_precision == "bf16"
                 and N.gemm_supported(w.shape[0], w.shape[1]))
 
