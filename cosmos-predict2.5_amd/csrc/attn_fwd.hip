@@ -1212,6 +1212,11 @@ constexpr bool kPvFirst = CP25_M16_PV_FIRST;
 #define CP25_M16_LSUM_FIRST 0
 #endif
 constexpr bool kLsumFirst = CP25_M16_LSUM_FIRST;  // row-sum MFMAs at the MFMA phase's start (else after the P.V pairs)
+#ifndef CP25_M16_PRE_B
+#define CP25_M16_PRE_B 1
+#endif
+// group B issues its MFMA phase's first operand reads at the end of its softmax phase, before the barrier
+constexpr bool kPreB = CP25_M16_PRE_B;
 constexpr int kKBuf16 = kKBlk * kKStride16;        // 18432
 constexpr int kVBuf16 = kKBlk * kVStride16;        // 18432
 constexpr int kLds16 = 2 * kKBuf16 + 2 * kVBuf16;  // 73728
@@ -1408,17 +1413,16 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
   // Operand pair n (one fragment, two MFMAs, one per query half): n < 16 the K fragment (kb = n & 3, s = n >> 2),
   // n >= 16 the V^T fragment (db = (n - 16) & 7, ks = (n - 16) >> 3). Reads are inline asm issued kAhead pairs
   // ahead into a (kAhead + 1)-deep ring, each pair preceded by a counted lgkmcnt wait naming its operand.
-  auto mfma_phase = [&](auto PAR) __attribute__((always_inline)) {
-    constexpr int par = decltype(PAR)::value;
-    constexpr int kbuf = (par ^ 1) ? KB1 : 0;  // K(t+1)
-    constexpr int vbuf = par ? kVBuf16 : 0;    // V(t), relative to VB0
-    constexpr int kR = kAhead + 1;
-    bf16x8 ring[kR];
+  constexpr int kR = kAhead + 1;
+  bf16x8 ring[kR];  // operand ring of the MFMA phase (group B may fill its head before the phase's barrier)
 #ifdef CP25_LAB_NOLDS
 #pragma unroll
-    for (int i = 0; i < kR; ++i) ring[i] = qf[1][i & 3];
+  for (int i = 0; i < kR; ++i) ring[i] = qf[1][i & 3];
 #endif
-    auto issue = [&](auto NC) __attribute__((always_inline)) {
+  auto issue_pair = [&](auto PAR, auto NC) __attribute__((always_inline)) {
+      constexpr int par = decltype(PAR)::value;
+      constexpr int kbuf = (par ^ 1) ? KB1 : 0;  // K(t+1)
+      constexpr int vbuf = par ? kVBuf16 : 0;    // V(t), relative to VB0
       constexpr int n = decltype(NC)::value;
 #ifdef CP25_LAB_NOLDS  // lab only (wrong results): the MFMA phase reads no LDS (operands stay in the ring)
       if constexpr (true) {
@@ -1438,7 +1442,11 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
         const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         ring[n % kR] = __builtin_bit_cast(bf16x8, r);
       }
-    };
+  };
+  // PRE: the first kAhead pairs were issued before the barrier that opens the phase (group B: its V(t) and K(t+1)
+  // were written at least one barrier earlier, so it may read them while finishing its softmax phase)
+  auto mfma_phase = [&](auto PAR, auto PRE) __attribute__((always_inline)) {
+    auto issue = [&](auto NC) __attribute__((always_inline)) { issue_pair(PAR, NC); };
     constexpr auto nreads = [](int n) constexpr {
 #ifdef CP25_LAB_NOLDS
       return 0 * n;
@@ -1447,7 +1455,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
     };
     __builtin_amdgcn_s_setprio(1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    static_for<kAhead>(issue);
+    if constexpr (!decltype(PRE)::value) static_for<kAhead>(issue);
     if constexpr (kLsum && kLsumFirst) {
       // the row-sum MFMAs need no LDS operand: they cover the first reads' latency at the phase start
 #pragma unroll
@@ -1498,7 +1506,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
     // group A: phase 2t MFMA, phase 2t+1 softmax(t+1) + V(t+1) staging
     auto step = [&](auto PAR, int t) __attribute__((always_inline)) {
       constexpr int par = decltype(PAR)::value;
-      mfma_phase(PAR);
+      mfma_phase(PAR, std::false_type{});
       ATTN_STAMP(t, 0);
       __syncthreads();
       ATTN_STAMP(t, 1);
@@ -1526,10 +1534,11 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
       softmax(t);
       ATTN_STAMP(t, 4);
       if (!kEarlyLoad && t + 2 < ntiles) load_tile(t + 3);
+      if constexpr (kPreB) static_for<kAhead>([&](auto NC) __attribute__((always_inline)) { issue_pair(PAR, NC); });
       ATTN_STAMP(t, 0);
       __syncthreads();
       ATTN_STAMP(t, 1);
-      mfma_phase(PAR);
+      mfma_phase(PAR, std::integral_constant<bool, kPreB>{});
       ATTN_STAMP(t, 2);
       __syncthreads();
       ATTN_STAMP(t, 3);
