@@ -61,6 +61,10 @@ SIGNATURES = {
     "cp25_attn_fwd_prescaled_fp8": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, _F, _F, _I,
                                     _P, ctypes.c_size_t, _P],
     "cp25_v_fp8t_bytes": [_I, _I, _I],
+    "cp25_v_bf16t_bytes": [_I, _I, _I],
+    "cp25_cast_v_bf16t": [_P, c_int64_p, _I, _I, _I, _I, _P, _P],
+    "cp25_attn_fwd_prescaled_vt": [_P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, _F, _F, _I,
+                                   _P, ctypes.c_size_t, _P],
     "cp25_cast_v_fp8t": [_P, c_int64_p, _I, _I, _I, _I, _P, _P, _P],
     "cp25_attn_workspace_bytes": [_I, _I, _I, _I],
     "cp25_attn_plan": [_I, _I, _I, _I, _I],
@@ -111,6 +115,7 @@ def load_library() -> ctypes.CDLL:
         if argtypes is not None:
             fn.argtypes = argtypes
         fn.restype = {"cp25_attn_workspace_bytes": ctypes.c_size_t, "cp25_v_fp8t_bytes": ctypes.c_int64,
+                          "cp25_v_bf16t_bytes": ctypes.c_int64,
                       "cp25_vae_attn_workspace_bytes": ctypes.c_int64}.get(name, ctypes.c_int)
     _lib = lib
     return lib
@@ -156,7 +161,8 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
              softmax_scale: Optional[float] = None, n_split: Optional[int] = None,
              norm_bounds: Optional[Tuple[float, float]] = None, prescaled: bool = False,
              fp8_qk: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-             fp8_v: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+             fp8_v: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+             v_t: Optional[torch.Tensor] = None) -> torch.Tensor:
     """softmax(q k^T * scale) v for q [B, Lq, H, 128], k/v [B, Lk, H, 128] (bf16, any strides with
     a contiguous head dim). Returns [B, Lq, H, 128] bf16. n_split: key-range split (None = the
     library's plan for this shape; the fp32 partials live in a caching-allocator workspace).
@@ -167,7 +173,9 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
     fp8_qk=(q8, k8): with prescaled, Q K^T runs on the e4m3 copies (uint8 views shaped like q / k, from
     cast_fp8(q * 2^s), cast_fp8(k * 2^-s); cp25_attn_fwd_prescaled_fp8qk); q / k are then only shape
     references. fp8_v=(v8t, v_amax) (with fp8_qk; from cast_v_fp8t(v)): P.V on e5m2 P and e4m3 V too
-    (cp25_attn_fwd_prescaled_fp8); v is then only a shape reference."""
+    (cp25_attn_fwd_prescaled_fp8); v is then only a shape reference. v_t (with prescaled, bf16; from
+    cast_v_bf16t(v)): V as the V^T tile layout, one LDS read per P.V operand (cp25_attn_fwd_prescaled_vt,
+    bit-identical to the plain form); v is then only a shape reference."""
     lib = load_library()
     if q.dtype != torch.bfloat16 or k.dtype != torch.bfloat16 or v.dtype != torch.bfloat16:
         raise ValueError("attn_fwd expects bf16 q/k/v (attention() recasts to bf16 first)")
@@ -215,6 +223,14 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
                                                    qb, kb, int(n_split), _ptr(ws), ws_bytes, _stream(q.device))
             _check("cp25_attn_fwd_prescaled_fp8qk", rc)
             return out
+        if v_t is not None:
+            if v_t.dtype != torch.bfloat16 or v_t.numel() * 2 != lib.cp25_v_bf16t_bytes(B, H, Lk):
+                raise ValueError("v_t: bf16 tensor of cp25_v_bf16t_bytes(B, H, Lk) bytes (cast_v_bf16t) expected")
+            rc = lib.cp25_attn_fwd_prescaled_vt(_ptr(q), _ptr(k), _ptr(v_t), _ptr(out), B, H, Lq, Lk, D, strides[0],
+                                                strides[1], strides[3], qb, kb, int(n_split), _ptr(ws), ws_bytes,
+                                                _stream(q.device))
+            _check("cp25_attn_fwd_prescaled_vt", rc)
+            return out
         rc = lib.cp25_attn_fwd_prescaled(_ptr(q), _ptr(k), _ptr(v), _ptr(out), B, H, Lq, Lk, D, *strides, qb, kb,
                                          int(n_split), _ptr(ws), ws_bytes, _stream(q.device))
         _check("cp25_attn_fwd_prescaled", rc)
@@ -246,6 +262,22 @@ def cast_v_fp8t(v: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
                               _ptr(amax), _stream(v.device))
     _check("cp25_cast_v_fp8t", rc)
     return v8t, amax
+
+
+def cast_v_bf16t(v: torch.Tensor) -> torch.Tensor:
+    """V^T tiles for attn_fwd(v_t=...): v bf16 [B, L, H, 128] (any strides, contiguous head dim) -> the layout of
+    cp25_cast_v_bf16t (an exact copy, keys permuted to the 16x16x32 P^T operand's order, zero past L)."""
+    lib = load_library()
+    if v.dtype != torch.bfloat16 or v.dim() != 4 or v.stride(3) != 1:
+        raise ValueError("cast_v_bf16t expects bf16 [B, L, H, 128] with a contiguous head dim")
+    B, L, H, D = v.shape
+    n = lib.cp25_v_bf16t_bytes(B, H, L)
+    _check("cp25_v_bf16t_bytes", min(n, 0))
+    vt = torch.empty((n // 2,), dtype=torch.bfloat16, device=v.device)
+    rc = lib.cp25_cast_v_bf16t(_ptr(v), _i64x3((v.stride(0), v.stride(1), v.stride(2))), B, H, L, D, _ptr(vt),
+                               _stream(v.device))
+    _check("cp25_cast_v_bf16t", rc)
+    return vt
 
 
 def cast_fp8(src: torch.Tensor, scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -212,6 +212,8 @@ class MinimalV1LVGDiT:
         self.attention_precision = "bf16"
         # the CFG pair's shared block-0 prefix runs once (see _blocks); False: every entry computes it
         self.share_cfg_block0 = True
+        # bf16 prescaled self-attention reads V from the V^T tile layout when CP25_ATTN_VT=1 (default: the qkv buffer)
+        self.attn_vt = os.environ.get("CP25_ATTN_VT", "0") != "0"
         # MLP layer1 + GELU: "lib" (default) = hipBLASLt + cp25_gelu, "own" = cp25_gemm_epi with the GELU epilogue
         # (measured 0.25 % slower end to end: 0.7264 vs 0.7282 frames/s, profiles/r2/gemm_gelu/)
         self.mlp1_gemm = os.environ.get("CP25_MLP1_GEMM", "lib")
@@ -242,11 +244,16 @@ class MinimalV1LVGDiT:
 
     def _fp8_qk(self, q_cols: torch.Tensor, k_cols: torch.Tensor, B: int, H: int, hd: int, attn_kw: dict,
                 v: Optional[torch.Tensor] = None):
-        """attn_fwd kwargs for the fp8 forms: e4m3 [n, B, H, hd] copies of the q / k columns (2-D row views of
-        the token-major qkv / gathered kv buffers), transposed like the bf16 views; "fp8" also the e4m3 V^T
-        tiles of v ([B, L, H, hd] view)."""
-        if self.attention_precision == "bf16" or not attn_kw.get("prescaled"):
+        """attn_fwd kwargs of the prescaled self-attention beyond the bf16 views: bf16, the V^T tiles of v
+        ([B, L, H, hd] view; cp25_cast_v_bf16t); fp8 forms, e4m3 [n, B, H, hd] copies of the q / k columns (2-D
+        row views of the token-major qkv / gathered kv buffers), transposed like the bf16 views, and for "fp8"
+        also the e4m3 V^T tiles of v."""
+        if not attn_kw.get("prescaled"):
             return attn_kw
+        if self.attention_precision == "bf16":
+            # V^T tiles (one exact copy of v, 0.25 % of the launch): the 16x16x32 kernel's P.V operand becomes one
+            # ds_read_b128 instead of two transposed reads (cp25_attn_fwd_prescaled_vt, bit-identical output)
+            return dict(attn_kw, v_t=N.cast_v_bf16t(v)) if self.attn_vt and v is not None else attn_kw
         q8 = N.cast_fp8(q_cols, 4.0).view(-1, B, H, hd).transpose(0, 1)
         k8 = N.cast_fp8(k_cols, 0.25).view(-1, B, H, hd).transpose(0, 1)
         kw = dict(attn_kw, fp8_qk=(q8, k8))

@@ -1220,16 +1220,23 @@ constexpr bool kPreB = CP25_M16_PRE_B;
 constexpr int kKBuf16 = kKBlk * kKStride16;        // 18432
 constexpr int kVBuf16 = kKBlk * kVStride16;        // 18432
 constexpr int kLds16 = 2 * kKBuf16 + 2 * kVBuf16;  // 73728
+// kVt (cp25_attn_fwd_prescaled_vt): V arrives as cp25_cast_v_bf16t's V^T tiles ([128 d][64 p], 16 KiB contiguous),
+// LDS rows of 160 B (128 + 32): the fragment read (row 16 db + c, 16-B chunk 4 ks + g) lands on slot
+// (10 c + g + 4 ks) mod 16, distinct within every ds_read_b128 lane group
+constexpr int kVtStride = 160;
+constexpr int kVtBuf = kD * kVtStride;             // 20480
+constexpr int kLds16t = 2 * kKBuf16 + 2 * kVtBuf;  // 77824
 
 __device__ __forceinline__ float group4_sum(float x) {  // sum over the 4 lane groups of 16 (lanes c, c+16, c+32, c+48)
   x += __shfl_xor(x, 16);
   return x + __shfl_xor(x, 32);
 }
 
-template <int kKind, bool kPre>
+template <int kKind, bool kPre, bool kVt = false>
 __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[kLds16];
+  __shared__ __attribute__((aligned(16))) char smem[kVt ? kLds16t : kLds16];
   constexpr int KB1 = kKBuf16, VB0 = 2 * kKBuf16;
+  constexpr int VBUF = kVt ? kVtBuf : kVBuf16;  // V buffer 1, relative to VB0
 
   const int nwg = gridDim.x;
   const int tile = xcd_remap(blockIdx.x, nwg);
@@ -1249,7 +1256,8 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
 
   const unsigned short* qp = a.q + b * a.q_sb + h * a.q_sh;
   const unsigned short* kp = a.k + b * a.k_sb + h * a.k_sh + (int64_t)key0 * a.k_sl;
-  const unsigned short* vp = a.v + b * a.v_sb + h * a.v_sh + (int64_t)key0 * a.v_sl;
+  const unsigned short* vp = kVt ? (const unsigned short*)((const char*)a.v + ((int64_t)bh * a.ntk_v + key0 / kKBlk) * 16384)
+                                 : a.v + b * a.v_sb + h * a.v_sh + (int64_t)key0 * a.v_sl;
 
   // ---- Q fragments (B operand): Q[16 qh + c][32 s + 8 g .. +7] ----
   int q_row[2];
@@ -1290,41 +1298,45 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
   const int ntiles = (Lk + kKBlk - 1) / kKBlk;
 
   // staging (as attn_fwd_d128): a group's 256 threads own rows u/16 + 16 i, chunk u%16 of a 64 x 128 tile
+  // (kVt, group A: rows u/8 + 32 i, chunk u%8 of the 128 x 64 V^T tile, 16 KiB contiguous)
   const int u = tid & (kThreads / 2 - 1);
-  const int srow = u >> 4, sch = u & 15;
-  const int64_t sl = group_b ? a.k_sl : a.v_sl;
+  const bool vt_stage = kVt && !group_b;
+  const int srow = vt_stage ? u >> 3 : u >> 4, sch = vt_stage ? u & 7 : u & 15;
+  const int64_t sl = group_b ? a.k_sl : (kVt ? 64 : a.v_sl);
   const char* sbase = group_b ? (const char*)kp : (const char*)vp;
-  const int st_off = (int)(srow * sl * 2) + sch * 16, st_step = (int)(16 * sl * 2);
+  const int st_off = (int)(srow * sl * 2) + sch * 16, st_step = (int)((vt_stage ? 32 : 16) * sl * 2);
   u32x4 st[4];
   auto load_tile = [&](int t) __attribute__((always_inline)) {
     const int rows = min(Lk - t * kKBlk, kKBlk);
-    const int nbytes = rows > 0 ? (int)((rows - 1) * sl * 2) + 2 * kD : 0;
+    const int nbytes = vt_stage ? (rows > 0 ? 16384 : 0) : (rows > 0 ? (int)((rows - 1) * sl * 2) + 2 * kD : 0);
 #ifdef CP25_LAB_TILE0  // lab only (wrong results): every tile re-reads key tile 0 (cache-resident K/V stream)
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)sbase, (short)0, nbytes, 0x00020000);
 #else
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(sbase + (int64_t)t * kKBlk * sl * 2), (short)0,
-                                                        nbytes, 0x00020000);
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(sbase + (int64_t)t * (vt_stage ? 16384 : kKBlk * sl * 2)), (short)0, nbytes, 0x00020000);
 #endif
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       st[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, st_off + i * st_step, 0, 0));
   };
   char* const k_wr = smem + srow * kKStride16 + sch * 16;
-  char* const v_wr = smem + VB0 + srow * kVStride16 + sch * 16;
+  char* const v_wr = smem + VB0 + srow * (kVt ? kVtStride : kVStride16) + sch * 16;
   auto write_k = [&](auto BUF) __attribute__((always_inline)) {
     constexpr int kb = decltype(BUF)::value ? KB1 : 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(k_wr + kb + 16 * i * kKStride16) = st[i];
   };
   auto write_v = [&](auto BUF) __attribute__((always_inline)) {
-    constexpr int vb = decltype(BUF)::value ? kVBuf16 : 0;
+    constexpr int vb = decltype(BUF)::value ? VBUF : 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(v_wr + vb + 16 * i * kVStride16) = st[i];
+    for (int i = 0; i < 4; ++i)
+      *reinterpret_cast<u32x4*>(v_wr + vb + (kVt ? 32 * i * kVtStride : 16 * i * kVStride16)) = st[i];
   };
 
   // per-lane LDS read bases; everything else is an immediate offset
   const char* const k_rd = smem + c16 * kKStride16 + 16 * g;  // + KB + 16 kb rows + 64 s bytes
-  const char* const v_rd = smem + VB0 + (4 * g + (c16 >> 2)) * kVStride16 + 8 * (c16 & 3);  // + VB + rows + 32 db
+  const char* const v_rd = kVt ? smem + VB0 + c16 * kVtStride + 16 * g  // + VB + 16 db rows + 64 ks bytes
+                               : smem + VB0 + (4 * g + (c16 >> 2)) * kVStride16 + 8 * (c16 & 3);  // + VB + rows + 32 db
   const unsigned k_rd_lds = (unsigned)(uintptr_t)(lds_char_ptr)k_rd;
   const unsigned v_rd_lds = (unsigned)(uintptr_t)(lds_char_ptr)v_rd;
 
@@ -1422,7 +1434,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
   auto issue_pair = [&](auto PAR, auto NC) __attribute__((always_inline)) {
       constexpr int par = decltype(PAR)::value;
       constexpr int kbuf = (par ^ 1) ? KB1 : 0;  // K(t+1)
-      constexpr int vbuf = par ? kVBuf16 : 0;    // V(t), relative to VB0
+      constexpr int vbuf = par ? VBUF : 0;       // V(t), relative to VB0
       constexpr int n = decltype(NC)::value;
 #ifdef CP25_LAB_NOLDS  // lab only (wrong results): the MFMA phase reads no LDS (operands stay in the ring)
       if constexpr (true) {
@@ -1432,8 +1444,17 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
         constexpr int m = kPvFirst ? n - 16 : n;
         constexpr int off = kbuf + (m & 3) * 16 * kKStride16 + 64 * (m >> 2);
         asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ring[n % kR]) : "v"(k_rd_lds), "i"(off));
+      } else if constexpr (kVt && n < 32) {
+        constexpr int m = kPvFirst ? n : n - 16;  // db = m & 7, ks = m >> 3
+        constexpr int off = vbuf + 16 * (m & 7) * kVtStride + 64 * (m >> 3);
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ring[n % kR]) : "v"(v_rd_lds), "i"(off));
       } else if constexpr (n < 32) {
         constexpr int m = kPvFirst ? n : n - 16;
+#ifdef CP25_LAB_VB128  // lab only (wrong results): one ds_read_b128 per V^T fragment instead of two transposed reads
+        constexpr int offb = vbuf + 32 * (m >> 3) * kVStride16 + 32 * (m & 7) - VB0;
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ring[n % kR]) : "v"(k_rd_lds), "i"(VB0 + offb));
+        return;
+#endif
         constexpr int off = vbuf + 32 * (m >> 3) * kVStride16 + 32 * (m & 7);
         s16x4 lo, hi;
         asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(v_rd_lds), "i"(off));
@@ -1451,7 +1472,10 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
 #ifdef CP25_LAB_NOLDS
       return 0 * n;
 #endif
-      return n >= 32 ? 0 : ((kPvFirst ? n >= 16 : n < 16) ? 1 : 2);
+#ifdef CP25_LAB_VB128
+      return n >= 32 ? 0 : 1;
+#endif
+      return n >= 32 ? 0 : ((kVt || (kPvFirst ? n >= 16 : n < 16)) ? 1 : 2);
     };
     __builtin_amdgcn_s_setprio(1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1664,7 +1688,9 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
                        const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
                        const int64_t* o_strides, float softmax_scale, float q_norm_bound, float k_norm_bound,
                        int n_split, void* workspace, size_t ws_bytes, hipStream_t stream, bool prescaled = false,
-                       int fp8 = 0, const float* v_amax = nullptr) {
+                       int fp8 = 0, const float* v_amax = nullptr, bool vt = false) {
+  // vt: v is cp25_cast_v_bf16t's V^T tile layout (prescaled bf16 form on attn_fwd_m16 only; v_strides unused)
+  if (vt && (fp8 || !prescaled)) return CP25_ERR_INVAL;
   // fp8: 1 = Q K^T on e4m3 q / k; 2 = also P.V on e5m2 P and the e4m3 v8t layout (v = v8t, v_strides unused)
   const bool fp8qk = fp8 >= 1;
   if (D != kD) return CP25_ERR_DTYPE;
@@ -1681,12 +1707,12 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
   const int64_t* ss[4] = {q_strides, k_strides, v_strides, o_strides};
   for (int i = 0; i < 4; ++i)
     for (int j = 0; j < 3; ++j)
-      if (!(fp8 == 2 && i == 2) && ss[i][j] % (fp8qk && i < 2 ? 16 : 8) != 0) return CP25_ERR_INVAL;  // 16 B rows
+      if (!((fp8 == 2 || vt) && i == 2) && ss[i][j] % (fp8qk && i < 2 ? 16 : 8) != 0) return CP25_ERR_INVAL;  // 16 B rows
   // buffer_load offsets within a 64-key tile are 32-bit
   if ((int64_t)kKBlk * k_strides[1] * (fp8qk ? 1 : 2) >= (1ll << 31) ||
-      (fp8 != 2 && (int64_t)kKBlk * v_strides[1] * 2 >= (1ll << 31)))
+      (fp8 != 2 && !vt && (int64_t)kKBlk * v_strides[1] * 2 >= (1ll << 31)))
     return CP25_ERR_INVAL;
-  if (k_strides[1] <= 0 || (fp8 != 2 && v_strides[1] <= 0)) return CP25_ERR_INVAL;
+  if (k_strides[1] <= 0 || (fp8 != 2 && !vt && v_strides[1] <= 0)) return CP25_ERR_INVAL;
   if (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) & 15) return CP25_ERR_INVAL;
   const int64_t ntiles = cdiv(Lk, kKBlk);
   if (n_split < 1 || n_split > ntiles) return CP25_ERR_INVAL;
@@ -1751,6 +1777,9 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
     if (bhn * a.nchunk > 0x7fffffff) return CP25_ERR_INVAL;
     hipLaunchKernelGGL((attn_fwd_d128<1, true, true, false, true>), dim3((unsigned)(bhn * a.nchunk)), dim3(kThreads), 0,
                        stream, a);
+  } else if (vt) {
+    auto kernel = Lk <= 4096 ? attn_fwd_m16<1, true, true> : attn_fwd_m16<0, true, true>;
+    hipLaunchKernelGGL(kernel, dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
   } else if ((prescaled || fixed) && attn_m16()) {
     auto kernel = prescaled ? (Lk <= 4096 ? attn_fwd_m16<1, true> : attn_fwd_m16<0, true>)
                             : (Lk <= 4096 ? attn_fwd_m16<1, false> : attn_fwd_m16<0, false>);
@@ -1788,6 +1817,15 @@ extern "C" int cp25_attn_fwd_prescaled_fp8(const void* q8, const void* k8, const
   const int64_t none[3] = {0, 0, 0};
   return attn_launch(q8, k8, v8t, o, B, H, Lq, Lk, D, q_strides, k_strides, none, o_strides, 0.6931471805599453f,
                      q_norm_bound, k_norm_bound, n_split, workspace, ws_bytes, stream, true, 2, v_amax);
+}
+
+extern "C" int cp25_attn_fwd_prescaled_vt(const void* q, const void* k, const void* vt, void* o, int B, int H, int Lq,
+                                          int Lk, int D, const int64_t* q_strides, const int64_t* k_strides,
+                                          const int64_t* o_strides, float q_norm_bound, float k_norm_bound, int n_split,
+                                          void* workspace, size_t ws_bytes, hipStream_t stream) {
+  const int64_t none[3] = {0, 0, 0};
+  return attn_launch(q, k, vt, o, B, H, Lq, Lk, D, q_strides, k_strides, none, o_strides, 0.6931471805599453f,
+                     q_norm_bound, k_norm_bound, n_split, workspace, ws_bytes, stream, true, 0, nullptr, true);
 }
 
 extern "C" size_t cp25_attn_workspace_bytes(int B, int H, int Lq, int n_split) {

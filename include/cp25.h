@@ -91,6 +91,21 @@ int cp25_attn_fwd_prescaled_fp8qk(const void* q8, const void* k8, const void* v,
                                   const int64_t* o_strides, float q_norm_bound, float k_norm_bound, int n_split,
                                   void* workspace, size_t ws_bytes, hipStream_t stream);
 
+/* bf16 V^T tiles for cp25_attn_fwd_prescaled_vt: vt[b][h][tile][128 d][64 p] with p = 32 ks + 8 g + j holding
+ * V[32 ks + 16 (j >> 2) + 4 g + (j & 3)][d] (the key order of the 16x16x32 P^T operand), keys past L zero; an exact
+ * copy of v ([B, L, H, 128] by element strides, 16-B aligned rows). cp25_v_bf16t_bytes gives the vt size.
+ * Replaces: nothing in the reference (a layout of the V operand of networks/attention.py:90-181's softmax(QK^T)V). */
+int64_t cp25_v_bf16t_bytes(int B, int H, int L);
+int cp25_cast_v_bf16t(const void* v, const int64_t* v_strides, int B, int H, int L, int D, void* vt, hipStream_t stream);
+
+/* cp25_attn_fwd_prescaled with V given as cp25_cast_v_bf16t's vt instead of [B, L, H, 128] strides: the P.V operand
+ * is one ds_read_b128 per fragment instead of two transposed reads (16x16x32 kernel only); bit-identical output.
+ * Replaces: networks/attention.py:90-181 (attention(q, k, v)) as cp25_attn_fwd_prescaled does. */
+int cp25_attn_fwd_prescaled_vt(const void* q, const void* k, const void* vt, void* o, int B, int H, int Lq, int Lk,
+                               int D, const int64_t* q_strides, const int64_t* k_strides, const int64_t* o_strides,
+                               float q_norm_bound, float k_norm_bound, int n_split, void* workspace, size_t ws_bytes,
+                               hipStream_t stream);
+
 /* V for the fp8 P.V of cp25_attn_fwd_prescaled_fp8: v_amax[b * H + h] = max |v| over the head's L rows (float,
  * device memory, B * H entries), then v8t = e4m3(v * 448 / amax) laid out [B][H][ceil(L / 64)][128 d][64 key
  * bytes], the keys of each 64-key tile permuted to the order the kernel's P^T operand holds them (zero keys pad

@@ -145,3 +145,43 @@ def test_m16_full_metric_shape_query_slice(device, monkeypatch):
     assert max(err) <= TOL, max(err)
     oc = _run(monkeypatch, "16", lambda: N.attn_fwd(qs, k, torch.full_like(v, 0.75), norm_bounds=nb, prescaled=True))
     assert ((oc.float() - 0.75).abs() <= 0.75 * 2 ** -7).all()
+
+
+def _vt_reference(v):
+    """torch restatement of cp25_cast_v_bf16t: [B][H][tile][128 d][64 p], p = 32 ks + 8 g + j holding key
+    32 ks + 16 (j >> 2) + 4 g + (j & 3) of the tile, zero past L."""
+    B, L, H, D = v.shape
+    nt = (L + 63) // 64
+    vp = torch.zeros(B, nt * 64, H, D, dtype=v.dtype, device=v.device)
+    vp[:, :L] = v
+    p = torch.arange(64)
+    key = 32 * (p >> 5) + 16 * ((p & 7) >> 2) + 4 * ((p >> 3) & 3) + (p & 3)
+    t = vp.view(B, nt, 64, H, D)[:, :, key.to(v.device)]  # [B, nt, 64 p, H, D]
+    return t.permute(0, 3, 1, 4, 2).contiguous().view(-1)  # [B, H, nt, D, 64 p]
+
+
+@pytest.mark.parametrize("L", [64, 1000, 4097])
+def test_v_bf16t_layout_exact(device, L):
+    g = torch.Generator(device="cpu").manual_seed(L)
+    qkv = torch.randn(L, 2, 3, 4, 128, generator=g).to(device, torch.bfloat16)
+    v = qkv[:, :, 2].transpose(0, 1)  # strided [B, L, H, D] view of a token-major buffer
+    vt = N.cast_v_bf16t(v)
+    torch.cuda.synchronize()
+    assert torch.equal(vt, _vt_reference(v))
+
+
+@pytest.mark.parametrize("B,H,Lq,Lk,n_split", [(1, 1, 32, 64, 1), (2, 3, 300, 77, 1), (2, 2, 1000, 1030, 1),
+                                               (1, 2, 777, 3000, 3), (1, 2, 64, 4097, 5), (2, 4, 4800, 512, 1),
+                                               (1, 1, 5, 3, 1)])
+def test_m16_vt_bit_identical(device, monkeypatch, B, H, Lq, Lk, n_split):
+    """cp25_attn_fwd_prescaled_vt (V^T tiles, one ds_read_b128 per P.V operand) = cp25_attn_fwd_prescaled on the
+    16x16x32 kernel bit for bit: the same operand values in the same k order."""
+    q, k, v = _inputs(device, B, H, Lq, Lk, 77 + Lq + Lk)
+    c = 128 ** -0.5 * LOG2E
+    qs = (q.float() * c).to(torch.bfloat16)
+    nb = (qs.float().norm(dim=-1).max().item() * 1.01, k.float().norm(dim=-1).max().item())
+    vt = N.cast_v_bf16t(v)
+    o_vt = _run(monkeypatch, "16", lambda: N.attn_fwd(qs, k, v, norm_bounds=nb, prescaled=True, n_split=n_split,
+                                                      v_t=vt))
+    o = _run(monkeypatch, "16", lambda: N.attn_fwd(qs, k, v, norm_bounds=nb, prescaled=True, n_split=n_split))
+    assert torch.equal(o_vt, o)
