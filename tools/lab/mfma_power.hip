@@ -67,6 +67,64 @@ __global__ void __launch_bounds__(512, 2) mfma_loop16(const bf16x8* __restrict__
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// pattern 7 / 8: block-scaled fp8 (e4m3) MFMAs on random bytes, same 4096 outputs per wave:
+// 7 = v_mfma_scale_f32_32x32x64_f8f6f4 (4 accumulators of 32 x 32), 8 = v_mfma_scale_f32_16x16x128_f8f6f4 (16 of 16 x 16)
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+template <int P>
+__global__ void __launch_bounds__(512, 2) mfma_loop_f8(const i32x8* __restrict__ src, float* __restrict__ out, int iters) {
+  const int lane = threadIdx.x & 63;
+  i32x8 a[4], b[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    a[i] = src[(i * 64 + lane) % 512];
+    b[i] = src[((i + 4) * 64 + lane) % 512];
+  }
+  float s = 0.f;
+  if constexpr (P == 7) {
+    f32x16 acc[4] = {};
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int j = 0; j < 32; ++j)
+        acc[j & 3] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a[j & 3], b[(j >> 2) & 3], acc[j & 3], 0, 0, 0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s += acc[c][r];
+  } else {
+    f32x4 acc[16] = {};
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int j = 0; j < 64; ++j)
+        acc[j & 15] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[j & 3], b[(j >> 1) & 3], acc[j & 15], 0, 0, 0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int c = 0; c < 16; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s += acc[c][r];
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+template <int P>
+double run_f8(const i32x8* src, float* out, int iters) {
+  const int grid = 256 * 2, block = 512;
+  hipLaunchKernelGGL(mfma_loop_f8<P>, dim3(grid), dim3(block), 0, 0, src, out, 10);
+  hipDeviceSynchronize();
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  hipEventRecord(e0);
+  hipLaunchKernelGGL(mfma_loop_f8<P>, dim3(grid), dim3(block), 0, 0, src, out, iters);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, e0, e1);
+  // per iteration and wave: 32 x (32 x 32 x 64) or 64 x (16 x 16 x 128) MACs = the same 2^21
+  const double flop = 2.0 * 32 * 32 * 64 * 32.0 * iters * (grid * block / 64);
+  return flop / (ms * 1e-3) / 1e12;
+}
+
 template <int P>
 double run(const bf16x8* src, float* out, int iters) {
   const int grid = 256 * 2, block = 512;
@@ -102,6 +160,15 @@ int main(int argc, char** argv) {
   hipMalloc(&out, 256 * 2 * 512 * 4);
   hipMemcpy(src, h.data(), h.size() * 2, hipMemcpyHostToDevice);
   hipMemset(zsrc, 0, h.size() * 2);
+  // random e4m3 bytes (finite: exponent field below 15 keeps clear of NaN), 512 lanes x 32 B
+  std::vector<unsigned char> h8(512 * 32);
+  for (auto& v : h8) {
+    x = x * 1664525u + 1013904223u;
+    v = (unsigned char)(((x >> 31) << 7) | ((((x >> 20) % 6) + 4) << 3) | ((x >> 8) & 7));
+  }
+  void* src8;
+  hipMalloc(&src8, h8.size());
+  hipMemcpy(src8, h8.data(), h8.size(), hipMemcpyHostToDevice);
   for (int rep = 0; rep < 2; ++rep) {
     printf("pattern 0 (A, B change every MFMA): %.1f TFLOP/s\n", run<0>(src, out, iters));
     printf("pattern 1 (A every MFMA, B every 8): %.1f TFLOP/s\n", run<1>(src, out, iters));
@@ -111,6 +178,10 @@ int main(int argc, char** argv) {
     printf("pattern 5 (16x16x32, A, B change every MFMA): %.1f TFLOP/s\n", run<5>(src, out, iters));
     printf("pattern 6 (16x16x32, zero data): %.1f TFLOP/s\n", run<6>(zsrc, out, iters));
     printf("pattern 0 again: %.1f TFLOP/s\n", run<0>(src, out, iters));
+    printf("pattern 7 (fp8 32x32x64, random): %.1f TFLOP/s\n", run_f8<7>((const i32x8*)src8, out, iters));
+    printf("pattern 8 (fp8 16x16x128, random): %.1f TFLOP/s\n", run_f8<8>((const i32x8*)src8, out, iters));
+    printf("pattern 7z (fp8 32x32x64, zeros): %.1f TFLOP/s\n", run_f8<7>((const i32x8*)zsrc, out, iters));
+    printf("pattern 8z (fp8 16x16x128, zeros): %.1f TFLOP/s\n", run_f8<8>((const i32x8*)zsrc, out, iters));
     fflush(stdout);
   }
   return 0;
