@@ -1212,6 +1212,10 @@ constexpr bool kPvFirst = CP25_M16_PV_FIRST;
 #define CP25_M16_LSUM_FIRST 0
 #endif
 constexpr bool kLsumFirst = CP25_M16_LSUM_FIRST;  // row-sum MFMAs at the MFMA phase's start (else after the P.V pairs)
+#ifndef CP25_M16_LSUM_SOFTMAX
+#define CP25_M16_LSUM_SOFTMAX 0
+#endif
+constexpr bool kLsumSoftmax = CP25_M16_LSUM_SOFTMAX;  // row-sum MFMAs at the end of the softmax phase instead
 #ifndef CP25_M16_PRE_B
 #define CP25_M16_PRE_B 1
 #endif
@@ -1401,6 +1405,14 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
       if constexpr (!kLsum) l_run[qh] += psum;
     }
     asm volatile("" ::"v"(pb[0][0]), "v"(pb[0][1]), "v"(pb[1][0]), "v"(pb[1][1]), "v"(l_run[0]), "v"(l_run[1]));
+    if constexpr (kLsum && kLsumSoftmax) {
+      // the row-sum MFMAs in the softmax phase: they fill the partner wave's MFMA-pipe gaps (it waits on LDS
+      // operands) instead of lengthening this wave's MFMA phase, the critical one
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) lsum[qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones8, pb[ks][qh], lsum[qh], 0, 0, 0);
+    }
   };
 
   typedef std::integral_constant<int, 0> B0;
@@ -1480,7 +1492,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
     __builtin_amdgcn_s_setprio(1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if constexpr (!decltype(PRE)::value) static_for<kAhead>(issue);
-    if constexpr (kLsum && kLsumFirst) {
+    if constexpr (kLsum && !kLsumSoftmax && kLsumFirst) {
       // the row-sum MFMAs need no LDS operand: they cover the first reads' latency at the phase start
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
@@ -1510,7 +1522,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
       }
       // program order = issue order: read n + kAhead, wait, the pair's two MFMAs (the scheduler otherwise sinks
       // MFMAs below later reads and renames accumulators, which costs v_mov copies)
-      if constexpr (kLsum && !kLsumFirst && kPvFirst && n == 15) {
+      if constexpr (kLsum && !kLsumSoftmax && !kLsumFirst && kPvFirst && n == 15) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -1518,7 +1530,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
       }
       if constexpr (kM16Sched) __builtin_amdgcn_sched_barrier(0);
     });
-    if constexpr (kLsum && !kLsumFirst && !kPvFirst) {
+    if constexpr (kLsum && !kLsumSoftmax && !kLsumFirst && !kPvFirst) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
