@@ -1478,6 +1478,8 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
   };
   // PRE: the first kAhead pairs were issued before the barrier that opens the phase (group B: its V(t) and K(t+1)
   // were written at least one barrier earlier, so it may read them while finishing its softmax phase)
+  int probe_t = 0;  // lab probe: the tile of the running MFMA phase (read only by ATTN_STAMP under CP25_ATTN_PROBE)
+  (void)probe_t;
   auto mfma_phase = [&](auto PAR, auto PRE) __attribute__((always_inline)) {
     auto issue = [&](auto NC) __attribute__((always_inline)) { issue_pair(PAR, NC); };
     constexpr auto nreads = [](int n) constexpr {
@@ -1529,6 +1531,11 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
           for (int qh = 0; qh < 2; ++qh) lsum[qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones8, pb[ks][qh], lsum[qh], 0, 0, 0);
       }
       if constexpr (kM16Sched) __builtin_amdgcn_sched_barrier(0);
+#ifdef CP25_ATTN_PROBE
+      // lab probe: inside the MFMA phase, after the first operand pair (6) and after the P.V half (7)
+      if constexpr (n == 0) ATTN_STAMP(probe_t, 6);
+      if constexpr (n == 15) ATTN_STAMP(probe_t, 7);
+#endif
     });
     if constexpr (kLsum && !kLsumSoftmax && !kLsumFirst && !kPvFirst) {
 #pragma unroll
@@ -1542,6 +1549,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
     // group A: phase 2t MFMA, phase 2t+1 softmax(t+1) + V(t+1) staging
     auto step = [&](auto PAR, int t) __attribute__((always_inline)) {
       constexpr int par = decltype(PAR)::value;
+      probe_t = t;
       mfma_phase(PAR, std::false_type{});
       ATTN_STAMP(t, 0);
       __syncthreads();
@@ -1574,6 +1582,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
       ATTN_STAMP(t, 0);
       __syncthreads();
       ATTN_STAMP(t, 1);
+      probe_t = t;
       mfma_phase(PAR, std::integral_constant<bool, kPreB>{});
       ATTN_STAMP(t, 2);
       __syncthreads();

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--t0", type=int, default=200)
     ap.add_argument("--bounded", action="store_true", help="RMS-normed q/k + cp25_attn_fwd_bounded (the DiT's form)")
     ap.add_argument("--prescaled", action="store_true", help="RMS-normed k, q * scale * log2(e) + cp25_attn_fwd_prescaled")
+    ap.add_argument("--vt", action="store_true", help="with --prescaled: V as cp25_cast_v_bf16t tiles (_prescaled_vt)")
     ap.add_argument("--lib", default=os.path.join(ROOT, "tools", "lab", "libattn_probe.so"))
     a = ap.parse_args()
     lib = ctypes.CDLL(a.lib)
@@ -37,6 +38,13 @@ def main():
     lib.cp25_attn_fwd_prescaled.argtypes = [P, P, P, P] + [ctypes.c_int] * 5 + [P] * 4 + [ctypes.c_float] * 2 + \
         [ctypes.c_int, P, ctypes.c_size_t, P]
     lib.cp25_attn_fwd_prescaled.restype = ctypes.c_int
+    lib.cp25_attn_fwd_prescaled_vt.argtypes = [P, P, P, P] + [ctypes.c_int] * 5 + [P] * 3 + [ctypes.c_float] * 2 + \
+        [ctypes.c_int, P, ctypes.c_size_t, P]
+    lib.cp25_attn_fwd_prescaled_vt.restype = ctypes.c_int
+    lib.cp25_v_bf16t_bytes.argtypes = [ctypes.c_int] * 3
+    lib.cp25_v_bf16t_bytes.restype = ctypes.c_int64
+    lib.cp25_cast_v_bf16t.argtypes = [P, P] + [ctypes.c_int] * 4 + [P, P]
+    lib.cp25_cast_v_bf16t.restype = ctypes.c_int
     lib.cp25_attn_probe_set.argtypes = [P, ctypes.c_int]
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
@@ -56,8 +64,19 @@ def main():
     st = [strides(t) for t in (q, k, v, o)]
     stream = torch.cuda.current_stream().cuda_stream
 
+    vt = None
+    if a.vt:
+        vt = torch.empty(lib.cp25_v_bf16t_bytes(a.B, a.H, a.L) // 2, dtype=torch.bfloat16, device=dev)
+        assert lib.cp25_cast_v_bf16t(v.data_ptr(), ctypes.cast(st[2], P), a.B, a.H, a.L, 128, vt.data_ptr(),
+                                     stream) == 0
+
     def run():
-        if a.prescaled:
+        if a.vt:
+            nb = 128 ** 0.5 * 1.02
+            rc = lib.cp25_attn_fwd_prescaled_vt(q.data_ptr(), k.data_ptr(), vt.data_ptr(), o.data_ptr(), a.B, a.H, a.L,
+                                                a.L, 128, ctypes.cast(st[0], P), ctypes.cast(st[1], P),
+                                                ctypes.cast(st[3], P), nb * c, nb, 1, None, 0, stream)
+        elif a.prescaled:
             nb = 128 ** 0.5 * 1.02
             rc = lib.cp25_attn_fwd_prescaled(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), a.B, a.H, a.L, a.L,
                                              128, *[ctypes.cast(s, P) for s in st], nb * c, nb, 1, None, 0, stream)
@@ -101,6 +120,14 @@ def main():
         else:  # stamps 3 (previous tile) -> write_k, softmax -> 4 -> load_tile -> 0
             d["write_softmax"] = (t[:, :, 1:, 4] - t[:, :, :-1, 3]).mean()
             d["load_issue"] = (t[:, :, 1:, 0] - t[:, :, 1:, 4]).mean()
+        # 16x16x32 kernel (stamps 6 / 7 inside the MFMA phase): phase start -> first pair, P.V half, Q K^T half
+        if name == "A":
+            d["mfma_first_pair"] = (t[:, :, 1:, 6] - t[:, :, :-1, 3]).mean()
+        else:
+            d["mfma_first_pair"] = (t[..., 6] - t[..., 1]).mean()
+        d["mfma_pv_rest"] = (t[..., 7] - t[..., 6]).mean()
+        end = t[..., 0] if name == "A" else t[..., 2]
+        d["mfma_qk_half"] = (end - t[..., 7]).mean()
         res[name] = {k: round(float(x), 1) for k, x in d.items()}
     res["note"] = ("A: ph1 = MFMA phase, ph2 = softmax; B: ph1 = softmax, ph2 = MFMA (cycles of s_memtime); "
                    "write_softmax / load_issue split the softmax phase")
