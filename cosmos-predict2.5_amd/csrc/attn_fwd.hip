@@ -56,7 +56,6 @@ constexpr int kKStride = 272;
 constexpr int kVStride = 320;
 constexpr int kVBuf = kKBlk * kVStride;  // 20480
 constexpr int kKBuf = kKBlk * kKStride;  // 17408
-constexpr int kK0 = 0, kK1 = kKBuf, kV0 = 2 * kKBuf, kV1 = 2 * kKBuf + kVBuf;
 constexpr int kLdsBytes = 2 * kVBuf + 2 * kKBuf;  // 75776
 
 typedef __attribute__((address_space(3))) s16x4* lds_s16x4_ptr;
