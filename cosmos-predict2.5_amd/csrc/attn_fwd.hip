@@ -1242,7 +1242,12 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
   constexpr int VBUF = kVt ? kVtBuf : kVBuf16;  // V buffer 1, relative to VB0
 
   const int nwg = gridDim.x;
+#ifdef CP25_LAB_NOREMAP  // lab: dispatch order = tile order (all XCDs on the same (b, h) at a time)
+  const int tile = blockIdx.x;
+  (void)nwg;
+#else
   const int tile = xcd_remap(blockIdx.x, nwg);
+#endif
   const int qb = tile % a.nqb;
   const int bhs = tile / a.nqb;
   const int split = bhs % a.nsplit, bh = bhs / a.nsplit;
