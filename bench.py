@@ -13,7 +13,7 @@ i.e. whole-video frames/s. Synthetic data: seeded random weights with the 2B sha
 conditioning image, N(0, 1) text embeddings [1, 512, 100352]. bf16 compute.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
-N > 1 (torchrun, one rank per GPU, RCCL): the video's token sequence is sharded context-parallel over
+N > 1 (one rank per GPU, RCCL; under torch.distributed.run, or started by bench.py itself when launched plainly): the video's token sequence is sharded context-parallel over
 the N ranks (K/V all-gather over xGMI), the decode is banded over the ranks; all ranks work on the
 same video (strong scaling). Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement").
 """
@@ -58,6 +58,15 @@ def parse():
     ap.add_argument("--attention-precision", default="bf16", choices=("bf16", "fp8qk", "fp8"),
                     help="fp8qk: self-attention Q K^T on e4m3 operands; fp8: also P.V on e5m2 P / e4m3 V (config 5's "
                          "option; not the metric)")
+    ap.add_argument("--norm-weights", default="",
+                    help="lo,hi: every q/k RMSNorm weight uniform in [lo, hi] (seeded) instead of the init's ones -- the "
+                         "attention then runs the form a trained checkpoint gets (the report names it)")
+    ap.add_argument("--whole-video", action="store_true",
+                    help="also time one whole video end to end (encode + all evaluations + decode) and report it next "
+                         "to the per-evaluation value")
+    ap.add_argument("--block-gemm", default="own", choices=("own", "lib"),
+                    help="bf16 block projections: own = the hand-written MFMA GEMM with fused GELU / gated-residual "
+                         "epilogues (default), lib = hipBLASLt + the elementwise kernels (A/B)")
     ap.add_argument("--no-cfg-share", action="store_true",
                     help="every CFG entry computes block 0's shared self-attention prefix (A/B of the sharing)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -104,13 +113,38 @@ class _Timer:
         return out, el
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """`python bench.py --gpus N` without a launcher: start the N ranks as one torch.distributed.run child (one
+    process per GPU, LOCAL_RANK = GPU index, rendezvous on 127.0.0.1, the reference's torchrun ->
+    examples/inference.py flow) and return its exit code. Called before anything touches the GPU; the parent
+    never execs."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        raise SystemExit(launch_ranks(a.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}: launch N>1 with torch.distributed.run")
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
     if a.steps < 1:
         raise SystemExit("--steps must be >= 1")
     _heartbeat(rank)
@@ -132,6 +166,14 @@ def main():
                                 linear_precision=a.linear_precision, attention_precision=a.attention_precision)
     model = pipe.model
     model.net.share_cfg_block0 = not a.no_cfg_share
+    model.net.block_gemm = a.block_gemm
+    if a.norm_weights:
+        lo, hi = (float(x) for x in a.norm_weights.split(","))
+        gw = torch.Generator(device=dev).manual_seed(7)
+        for k_, w_ in model.net.sd.items():
+            if k_.endswith(("q_norm.weight", "k_norm.weight")):
+                w_.copy_((lo + (hi - lo) * torch.rand(w_.shape, device=dev, generator=gw)).to(w_.dtype))
+        model.net.refresh_norm_bounds()
     karras = model.config.use_kerras_sigma_at_inference
     frames = model.tokenizer.get_pixel_num_frames(state_t)
     # conditioning "image": frame 0 random uint8, later frames zero (read_and_process_image layout)
@@ -176,6 +218,21 @@ def main():
         lat = run.latents()
         video, t_dec = timer(lambda: model.decode(lat))
         assert video.shape[2] == frames and torch.isfinite(video.float()).all()
+        del video
+        t_whole = None
+        if a.whole_video:
+            def whole():
+                g0 = model.encode_conditioning(batch["video"], 1, state_t)
+                r0 = model.begin_sampling(g0, batch["t5_text_embeddings"], batch["neg_t5_text_embeddings"],
+                                          state_shape=state_shape, num_conditional_frames=1, guidance=7, seed=0,
+                                          num_steps=a.num_steps)
+                while not r0.done:
+                    r0.step()
+                return model.decode(r0.latents())
+
+            vid_w, t_whole = timer(whole)
+            assert torch.isfinite(vid_w.float()).all()
+            del vid_w
 
     video_s = t_enc + t_setup + evals * t_step + t_dec
     # dominant kernel: self-attention flash kernel, HIP events on its launch stream around every
@@ -197,7 +254,7 @@ def main():
 
     if rank == 0:
         valid = (a.num_steps == 35 and a.frames == 121 and (h, w) == (704, 1280) and a.model == "2B/post-trained"
-                 and a.linear_precision == "bf16" and a.attention_precision == "bf16")
+                 and a.linear_precision == "bf16" and a.attention_precision == "bf16" and not a.norm_weights)
         # HBM bytes per self-attention launch: a static prior from the committed rocprofv3 PMC passes of
         # this kernel at this shape (tools/pmc_attn.sh; FETCH_SIZE x2 gfx950 correction + WRITE_SIZE),
         # not collected in this run; only the CP = 1 metric shape was measured, other shapes report null
@@ -222,7 +279,11 @@ def main():
                                                 ("fp8 (attention Q K^T)", a.attention_precision == "fp8qk"),
                                                 ("fp8 (attention Q K^T, P.V)", a.attention_precision == "fp8")) if on)
                      + " + bf16",
-            "data": "synthetic: seeded random 2B/VAE weights, random conditioning image, N(0,1) text embeddings",
+            "data": "synthetic: seeded random 2B/VAE weights, random conditioning image, N(0,1) text embeddings"
+                    + (f", q/k norm weights uniform in [{a.norm_weights}]" if a.norm_weights else ""),
+            "value_method": "per-evaluation timing: frames / (encode + setup + evals x mean timed evaluation + decode), "
+                            "each part timed in this run",
+            "whole_video": None if t_whole is None else {"seconds": t_whole, "frames_per_s": frames / t_whole},
             "config": {
                 "workload": f"Predict2.5-2B Image2World {h}x{w}x{frames}f ({a.model}), {a.num_steps} "
                             + (f"Karras UniPC steps ({evals} evals" if karras else f"shift-5 UniPC steps ({evals} evals")
@@ -240,6 +301,9 @@ def main():
                 "linear_precision": a.linear_precision,
                 "attention_precision": a.attention_precision,
                 "cfg_block0_shared": bool(net.share_cfg_block0),
+                "block_gemm": net.block_gemm,
+                "norm_weights": a.norm_weights or "ones (init)",
+                "attention_kernels": net.attention_kernels(state_t * (h // 16) * (w // 16)),
                 "metric_config": valid,
             },
             "roofline": {

@@ -61,12 +61,9 @@ SIGNATURES = {
     "cp25_attn_fwd_prescaled_fp8": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, _F, _F, _I,
                                     _P, ctypes.c_size_t, _P],
     "cp25_v_fp8t_bytes": [_I, _I, _I],
-    "cp25_v_bf16t_bytes": [_I, _I, _I],
-    "cp25_cast_v_bf16t": [_P, c_int64_p, _I, _I, _I, _I, _P, _P],
-    "cp25_attn_fwd_prescaled_vt": [_P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, _F, _F, _I,
-                                   _P, ctypes.c_size_t, _P],
     "cp25_cast_v_fp8t": [_P, c_int64_p, _I, _I, _I, _I, _P, _P, _P],
     "cp25_attn_workspace_bytes": [_I, _I, _I, _I],
+    "cp25_attn_kernel": [_I, _F, _F, _F, _I, _I],
     "cp25_attn_plan": [_I, _I, _I, _I, _I],
     "cp25_ln_mod": [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _P, _P, _I64, _I, _I, _I64, _I64, _F, _P],
     "cp25_ln_mod_fp8": [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _P, _P, _P, _I64, _I, _I, _I64, _I64, _F, _P],
@@ -76,6 +73,7 @@ SIGNATURES = {
     "cp25_copy_rows": [_P, _I64, _P, _I64, _I64, _I64, _P],
     "cp25_gelu": [_P, _I64, _P],
     "cp25_gemm_epi": [_P, _I64, _P, _I64, _P, _I64, _I, _I, _I, _I, _P],
+    "cp25_gemm_res": [_P, _I64, _P, _I64, _P, _I64, _I, _I, _I, _P, _I64, _I64, _P, _I64, _I64, _I, _I64, _I64, _P],
     "cp25_quant_fp8_rows": [_P, _P, _P, _I64, _I64, _P],
     "cp25_gelu_quant_fp8": [_P, _P, _P, _I64, _I64, _P],
     "cp25_patchify": [_P, _P, _P, _P, _P, _I64, _I64, _I64, _P],
@@ -115,7 +113,7 @@ def load_library() -> ctypes.CDLL:
         if argtypes is not None:
             fn.argtypes = argtypes
         fn.restype = {"cp25_attn_workspace_bytes": ctypes.c_size_t, "cp25_v_fp8t_bytes": ctypes.c_int64,
-                          "cp25_v_bf16t_bytes": ctypes.c_int64,
+                      "cp25_attn_kernel": ctypes.c_char_p,
                       "cp25_vae_attn_workspace_bytes": ctypes.c_int64}.get(name, ctypes.c_int)
     _lib = lib
     return lib
@@ -150,6 +148,19 @@ def _i64x3(vals) -> ctypes.Array:
 
 
 # ----------------------------------------------------------------------------- attention
+# Key-range split override, resolved once at import from CP25_ATTN_SPLIT (e.g. "1": never split, for bitwise
+# CP = N vs CP = 1 checks; unset: the library's plan); set_attn_split() changes it in-process.
+_ATTN_SPLIT: Optional[int] = int(os.environ["CP25_ATTN_SPLIT"]) if os.environ.get("CP25_ATTN_SPLIT") else None
+
+
+def set_attn_split(n: Optional[int]) -> Optional[int]:
+    """Force every attn_fwd call without an explicit n_split to use at most n key-range splits (None: the library's
+    plan). Returns the previous setting."""
+    global _ATTN_SPLIT
+    prev, _ATTN_SPLIT = _ATTN_SPLIT, (None if n is None else int(n))
+    return prev
+
+
 def attn_plan(B: int, H: int, Lq: int, Lk: int, D: int = 128) -> int:
     """Key-range split the library picks for this shape (cp25_attn_plan)."""
     n = load_library().cp25_attn_plan(B, H, Lq, Lk, D)
@@ -161,21 +172,19 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
              softmax_scale: Optional[float] = None, n_split: Optional[int] = None,
              norm_bounds: Optional[Tuple[float, float]] = None, prescaled: bool = False,
              fp8_qk: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-             fp8_v: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-             v_t: Optional[torch.Tensor] = None) -> torch.Tensor:
+             fp8_v: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
     """softmax(q k^T * scale) v for q [B, Lq, H, 128], k/v [B, Lk, H, 128] (bf16, any strides with
     a contiguous head dim). Returns [B, Lq, H, 128] bf16. n_split: key-range split (None = the
     library's plan for this shape; the fp32 partials live in a caching-allocator workspace).
-    norm_bounds: (max |q|, max |k|) upper bounds over all rows, enabling the bounded-shift softmax
-    where they are small enough (cp25_attn_fwd_bounded; None = online max only).
-    prescaled=True: q rows already carry scale * log2(e) (head_rmsnorm_rope(out_scale=...)), norm_bounds
-    are those of the scaled q and of k with product <= 60 (cp25_attn_fwd_prescaled; softmax_scale unused).
+    norm_bounds: (max |q|, max |k|) upper bounds over all rows: where max|q| max|k| (in log2 units) <= 80 the
+    rows use a fixed softmax shift, else (or None) an online row max (cp25_attn_fwd_bounded; any data).
+    prescaled=True: q rows already carry scale * log2(e) (head_rmsnorm_rope(out_scale=...)); norm_bounds (of the
+    scaled q and of k) optional as above (cp25_attn_fwd_prescaled; softmax_scale unused).
     fp8_qk=(q8, k8): with prescaled, Q K^T runs on the e4m3 copies (uint8 views shaped like q / k, from
-    cast_fp8(q * 2^s), cast_fp8(k * 2^-s); cp25_attn_fwd_prescaled_fp8qk); q / k are then only shape
-    references. fp8_v=(v8t, v_amax) (with fp8_qk; from cast_v_fp8t(v)): P.V on e5m2 P and e4m3 V too
-    (cp25_attn_fwd_prescaled_fp8); v is then only a shape reference. v_t (with prescaled, bf16; from
-    cast_v_bf16t(v)): V as the V^T tile layout, one LDS read per P.V operand (cp25_attn_fwd_prescaled_vt,
-    bit-identical to the plain form); v is then only a shape reference."""
+    cast_fp8(q * 2^s), cast_fp8(k * 2^-s); cp25_attn_fwd_prescaled_fp8qk; needs bounds with product <= 60); q / k
+    are then only shape references. fp8_v=(v8t, v_amax) (with fp8_qk; from cast_v_fp8t(v)): P.V on e5m2 P and
+    e4m3 V too (cp25_attn_fwd_prescaled_fp8; needs 1.13 x the bound product <= 30); v is then only a shape
+    reference."""
     lib = load_library()
     if q.dtype != torch.bfloat16 or k.dtype != torch.bfloat16 or v.dtype != torch.bfloat16:
         raise ValueError("attn_fwd expects bf16 q/k/v (attention() recasts to bf16 first)")
@@ -190,8 +199,7 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
         out = torch.empty((B, Lq, H, D), dtype=torch.bfloat16, device=q.device)
     scale = float(D) ** -0.5 if softmax_scale is None else float(softmax_scale)
     if n_split is None:
-        forced = os.environ.get("CP25_ATTN_SPLIT")  # e.g. "1": never split (bitwise CP=N vs CP=1 checks)
-        n_split = min(int(forced), (Lk + 63) // 64) if forced else attn_plan(B, H, Lq, Lk, D)
+        n_split = min(_ATTN_SPLIT, (Lk + 63) // 64) if _ATTN_SPLIT else attn_plan(B, H, Lq, Lk, D)
     ws_bytes = lib.cp25_attn_workspace_bytes(B, H, Lq, n_split)
     ws = torch.empty(((ws_bytes + 15) // 16 * 4,), dtype=torch.float32, device=q.device) if ws_bytes else None
     qb, kb = (0.0, 0.0) if norm_bounds is None else (float(norm_bounds[0]), float(norm_bounds[1]))
@@ -199,9 +207,9 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
         raise ValueError(f"norm_bounds must be >= 0, got {norm_bounds}")
     strides = [_i64x3((t.stride(0), t.stride(1), t.stride(2))) for t in (q, k, v, out)]
     if prescaled:
-        if qb * kb > 60.0 or qb <= 0.0 or kb <= 0.0:
-            raise ValueError(f"prescaled attention needs norm bounds with product <= 60, got {norm_bounds}")
         if fp8_qk is not None:
+            if qb * kb > 60.0 or qb <= 0.0 or kb <= 0.0:
+                raise ValueError(f"fp8 Q K^T needs norm bounds with product <= 60, got {norm_bounds}")
             q8, k8 = fp8_qk
             if q8.dtype != torch.uint8 or k8.dtype != torch.uint8 or q8.shape != q.shape or k8.shape != k.shape:
                 raise ValueError("fp8_qk: uint8 (e4m3 bit pattern) views shaped like q and k expected")
@@ -210,6 +218,8 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
             strides[0] = _i64x3((q8.stride(0), q8.stride(1), q8.stride(2)))
             strides[1] = _i64x3((k8.stride(0), k8.stride(1), k8.stride(2)))
             if fp8_v is not None:
+                if 1.13 * qb * kb > 30.0:
+                    raise ValueError(f"fp8 P.V needs 1.13 x the norm-bound product <= 30, got {norm_bounds}")
                 v8t, amax = fp8_v
                 if v8t.dtype != torch.uint8 or v8t.numel() != lib.cp25_v_fp8t_bytes(B, H, Lk) or \
                         amax.dtype != torch.float32 or amax.numel() < B * H:
@@ -222,14 +232,6 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
             rc = lib.cp25_attn_fwd_prescaled_fp8qk(_ptr(q8), _ptr(k8), _ptr(v), _ptr(out), B, H, Lq, Lk, D, *strides,
                                                    qb, kb, int(n_split), _ptr(ws), ws_bytes, _stream(q.device))
             _check("cp25_attn_fwd_prescaled_fp8qk", rc)
-            return out
-        if v_t is not None:
-            if v_t.dtype != torch.bfloat16 or v_t.numel() * 2 != lib.cp25_v_bf16t_bytes(B, H, Lk):
-                raise ValueError("v_t: bf16 tensor of cp25_v_bf16t_bytes(B, H, Lk) bytes (cast_v_bf16t) expected")
-            rc = lib.cp25_attn_fwd_prescaled_vt(_ptr(q), _ptr(k), _ptr(v_t), _ptr(out), B, H, Lq, Lk, D, strides[0],
-                                                strides[1], strides[3], qb, kb, int(n_split), _ptr(ws), ws_bytes,
-                                                _stream(q.device))
-            _check("cp25_attn_fwd_prescaled_vt", rc)
             return out
         rc = lib.cp25_attn_fwd_prescaled(_ptr(q), _ptr(k), _ptr(v), _ptr(out), B, H, Lq, Lk, D, *strides, qb, kb,
                                          int(n_split), _ptr(ws), ws_bytes, _stream(q.device))
@@ -247,6 +249,15 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
     return out
 
 
+def attn_kernel_name(Lk: int, softmax_scale: Optional[float] = None, norm_bounds=None, prescaled: bool = False,
+                     fp8: int = 0) -> str:
+    """The kernel form attn_fwd launches for these arguments (cp25_attn_kernel), e.g.
+    'attn_fwd_m16<self, prescaled, online max>'."""
+    qb, kb = (0.0, 0.0) if norm_bounds is None else (float(norm_bounds[0]), float(norm_bounds[1]))
+    sc = 128 ** -0.5 if softmax_scale is None else float(softmax_scale)
+    return load_library().cp25_attn_kernel(int(Lk), sc, qb, kb, int(prescaled), int(fp8)).decode()
+
+
 def cast_v_fp8t(v: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     """(v8t, v_amax) for attn_fwd(fp8_v=...): v bf16 [B, L, H, 128] (any strides, contiguous head dim) ->
     the e4m3 V^T tile layout and the per-(b, h) max |v| (cp25_cast_v_fp8t)."""
@@ -262,22 +273,6 @@ def cast_v_fp8t(v: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
                               _ptr(amax), _stream(v.device))
     _check("cp25_cast_v_fp8t", rc)
     return v8t, amax
-
-
-def cast_v_bf16t(v: torch.Tensor) -> torch.Tensor:
-    """V^T tiles for attn_fwd(v_t=...): v bf16 [B, L, H, 128] (any strides, contiguous head dim) -> the layout of
-    cp25_cast_v_bf16t (an exact copy, keys permuted to the 16x16x32 P^T operand's order, zero past L)."""
-    lib = load_library()
-    if v.dtype != torch.bfloat16 or v.dim() != 4 or v.stride(3) != 1:
-        raise ValueError("cast_v_bf16t expects bf16 [B, L, H, 128] with a contiguous head dim")
-    B, L, H, D = v.shape
-    n = lib.cp25_v_bf16t_bytes(B, H, L)
-    _check("cp25_v_bf16t_bytes", min(n, 0))
-    vt = torch.empty((n // 2,), dtype=torch.bfloat16, device=v.device)
-    rc = lib.cp25_cast_v_bf16t(_ptr(v), _i64x3((v.stride(0), v.stride(1), v.stride(2))), B, H, L, D, _ptr(vt),
-                               _stream(v.device))
-    _check("cp25_cast_v_bf16t", rc)
-    return vt
 
 
 def cast_fp8(src: torch.Tensor, scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -394,7 +389,7 @@ def gelu_(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
-EPI_NONE, EPI_GELU = 0, 1
+EPI_NONE, EPI_GELU, EPI_RES = 0, 1, 2
 
 
 def gemm_supported(N: int, K: int) -> bool:
@@ -419,6 +414,36 @@ def gemm_epi(a: torch.Tensor, w: torch.Tensor, epilogue: int = EPI_NONE, out: Op
     rc = lib.cp25_gemm_epi(_ptr(a), a.stride(0), _ptr(w), w.stride(0), _ptr(out), out.stride(0), M, N, K, int(epilogue),
                            _stream(a.device))
     _check("cp25_gemm_epi", rc)
+    return out
+
+
+def gemm_res(a: torch.Tensor, w: torch.Tensor, x: torch.Tensor, x_st: int, x_sb: int, gate: torch.Tensor, *, B: int,
+             tok0: int, hw: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[M, N] = bf16(x + bf16(gate * bf16(a[M, K] w[N, K]^T))) (cp25_gemm_res): the block's gated residual fused into
+    the projection. Row r of out / a is token r // B, batch entry r % B; x is read as x[tok * x_st + b * x_sb + col]
+    (x_sb = 0 broadcasts one row), gate is a bf16 [B', T, N] view (strides (sb, st, 1)) read at the row's frame
+    (tok0 + tok) // hw."""
+    lib = load_library()
+    if a.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or gate.dtype != torch.bfloat16:
+        raise ValueError("gemm_res expects bf16 operands")
+    if a.dim() != 2 or w.dim() != 2 or a.shape[1] != w.shape[1] or a.stride(1) != 1 or w.stride(1) != 1:
+        raise ValueError(f"gemm_res shapes a{tuple(a.shape)} w{tuple(w.shape)}: need [M, K] x [N, K], K contiguous")
+    M, K = a.shape
+    N = w.shape[0]
+    if gate.dim() != 3 or gate.shape[-1] != N or gate.stride(2) != 1 or gate.shape[0] < B:
+        raise ValueError(f"gemm_res gate {tuple(gate.shape)}: need a [B, T, {N}] view with a unit inner stride")
+    n_tok = M // B
+    _check_frames(gate, n_tok=n_tok, B=B, tok0=tok0, hw=hw)
+    if M % B or x.stride(-1) != 1 or \
+            (n_tok - 1) * x_st + (B - 1) * x_sb + N > x.untyped_storage().nbytes() // 2 - x.storage_offset():
+        raise ValueError("gemm_res: x does not cover the rows")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    if tuple(out.shape) != (M, N) or out.stride(1) != 1:
+        raise ValueError(f"gemm_res out {tuple(out.shape)} != ({M}, {N})")
+    rc = lib.cp25_gemm_res(_ptr(a), a.stride(0), _ptr(w), w.stride(0), _ptr(out), out.stride(0), M, N, K, _ptr(x), x_st,
+                           x_sb, _ptr(gate), gate.stride(0), gate.stride(1), B, tok0, hw, _stream(a.device))
+    _check("cp25_gemm_res", rc)
     return out
 
 

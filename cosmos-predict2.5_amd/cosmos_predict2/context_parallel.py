@@ -53,9 +53,24 @@ def all_gather_into(out: torch.Tensor, x: torch.Tensor, group) -> torch.Tensor:
 
 
 class _Done:
-    """Handle of a collective that already completed (gloo staging path)."""
+    """Handle of a collective that already completed (tools that substitute local copies for the gather)."""
 
     def wait(self) -> bool:
+        return True
+
+
+class _GlooDeferred:
+    """Handle of a gloo all-gather of device data still in flight (tests; several ranks sharing one GPU): the
+    shard was staged to host memory at issue, the gloo collective runs asynchronously, and wait() lands the
+    gathered bytes in `out` on the CURRENT stream, so `out` is written only after wait() -- the ordering RCCL's
+    async work gives the lanes of run_lanes (the other lane's block is queued between issue and wait)."""
+
+    def __init__(self, out: torch.Tensor, parts, work, w: int, row_shape):
+        self.out, self.parts, self.work, self.w, self.row_shape = out, parts, work, w, row_shape
+
+    def wait(self) -> bool:
+        self.work.wait()
+        self.out.view((self.w * self.parts[0].shape[0],) + self.row_shape).copy_(torch.cat(self.parts, 0))
         return True
 
 
@@ -63,10 +78,13 @@ def all_gather_into_async(out: torch.Tensor, x: torch.Tensor, group):
     """Asynchronous all_gather_into: returns a handle whose .wait() makes the CURRENT stream wait for
     the gather. With RCCL the gather runs on the process group's own stream, ordered after the work
     already queued on the current stream (so x is complete), and overlaps whatever the current
-    stream does next; the gloo path (tests) completes before returning."""
+    stream does next; the gloo path (tests) stages x to the host and completes the gather in wait()."""
     if dist.get_backend(group) == "gloo" and x.is_cuda:
-        all_gather_into(out, x, group)
-        return _Done()
+        w = dist.get_world_size(group)
+        xc = x.detach().contiguous().cpu()
+        parts = [torch.empty_like(xc) for _ in range(w)]
+        work = dist.all_gather(parts, xc, group=group, async_op=True)
+        return _GlooDeferred(out, parts, work, w, tuple(xc.shape[1:]))
     w = dist.get_world_size(group)
     return dist.all_gather_into_tensor(out.view((w * x.shape[0],) + tuple(x.shape[1:])), x.contiguous(),
                                        group=group, async_op=True)

@@ -6,9 +6,10 @@ re-designed for the sampler hot path:
 
 * token-major activations [tokens, B, D] (CFG cond/uncond as batch B = 2, batch inner), so a
   context-parallel shard is a contiguous token range and every GEMM is one [tokens*B, K] x [K, N];
-* all non-GEMM work of a block is HIP (libcp25.so): fused gated-residual + LayerNorm + AdaLN
-  modulate, per-head RMSNorm + 3D RoPE writing bf16 q/k in place in the fused QKV buffer, flash
-  attention reading q/k/v straight out of that buffer, exact GELU; plain GEMMs go to hipBLASLt;
+* every block op is HIP (libcp25.so): the six projections on a hand-written MFMA GEMM with fused epilogues
+  (exact GELU on MLP layer1; the gated residual on the output / cross-output / layer2 projections), LayerNorm +
+  AdaLN modulate, per-head RMSNorm + 3D RoPE writing bf16 q/k in place in the fused QKV buffer, flash attention
+  reading q/k/v straight out of that buffer; the embedders, AdaLN-LoRA and final linear stay on hipBLASLt;
 * everything that is constant across the 36 sampler steps is computed once: the crossattn_proj
   text projection, the cross-attention K/V of every block (per prompt), the RoPE cos/sin tables;
 * AdaLN modulation of all blocks in two batched fp32 GEMMs per forward (reference: fp32 autocast).
@@ -16,7 +17,6 @@ re-designed for the sampler hot path:
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
@@ -212,11 +212,11 @@ class MinimalV1LVGDiT:
         self.attention_precision = "bf16"
         # the CFG pair's shared block-0 prefix runs once (see _blocks); False: every entry computes it
         self.share_cfg_block0 = True
-        # bf16 prescaled self-attention reads V from the V^T tile layout when CP25_ATTN_VT=1 (default: the qkv buffer)
-        self.attn_vt = os.environ.get("CP25_ATTN_VT", "0") != "0"
-        # MLP layer1 + GELU: "lib" (default) = hipBLASLt + cp25_gelu, "own" = cp25_gemm_epi with the GELU epilogue
-        # (measured 0.25 % slower end to end: 0.7264 vs 0.7282 frames/s, profiles/r2/gemm_gelu/)
-        self.mlp1_gemm = os.environ.get("CP25_MLP1_GEMM", "lib")
+        # bf16 block projections: "own" (default) = the hand-written MFMA GEMM with fused epilogues (cp25_gemm_epi:
+        # QKV, cross-q; + exact GELU on MLP layer1; cp25_gemm_res: the gated residual fused into the output,
+        # cross-output and MLP layer2 projections, so each LN-mod reads the new x once); "lib" = hipBLASLt GEMMs with
+        # the GELU and the residuals in the elementwise kernels (the round-2 path, kept for A/B)
+        self.block_gemm = "own"
 
     def set_linear_precision(self, precision: str) -> None:
         """"bf16" (default, the reference's arithmetic) or "fp8": the 28 blocks' q/k/v, output, cross-q,
@@ -244,39 +244,40 @@ class MinimalV1LVGDiT:
 
     def _fp8_qk(self, q_cols: torch.Tensor, k_cols: torch.Tensor, B: int, H: int, hd: int, attn_kw: dict,
                 v: Optional[torch.Tensor] = None):
-        """attn_fwd kwargs of the prescaled self-attention beyond the bf16 views: bf16, the V^T tiles of v
-        ([B, L, H, hd] view; cp25_cast_v_bf16t); fp8 forms, e4m3 [n, B, H, hd] copies of the q / k columns (2-D
-        row views of the token-major qkv / gathered kv buffers), transposed like the bf16 views, and for "fp8"
-        also the e4m3 V^T tiles of v."""
-        if not attn_kw.get("prescaled"):
+        """attn_fwd kwargs of the prescaled self-attention beyond the bf16 views: the fp8 forms' e4m3 [n, B, H, hd]
+        copies of the q / k columns (2-D row views of the token-major qkv / gathered kv buffers), transposed like the
+        bf16 views, and for "fp8" also the e4m3 V^T tiles of v. Each fp8 form runs only where its fixed softmax
+        window holds every row (the library's rule: bound product <= 60 for fp8 Q K^T, 1.13 x it <= 30 for fp8 P.V,
+        whose e5m2 P spans 2^-15 .. 2^15); beyond that the next wider form runs (fp8 -> fp8qk -> bf16)."""
+        if not attn_kw.get("prescaled") or self.attention_precision == "bf16":
             return attn_kw
-        if self.attention_precision == "bf16":
-            # V^T tiles (one exact copy of v, 0.25 % of the launch): the 16x16x32 kernel's P.V operand becomes one
-            # ds_read_b128 instead of two transposed reads (cp25_attn_fwd_prescaled_vt, bit-identical output)
-            return dict(attn_kw, v_t=N.cast_v_bf16t(v)) if self.attn_vt and v is not None else attn_kw
+        qb, kb = attn_kw["norm_bounds"]
+        if qb * kb > 60.0:
+            return attn_kw
         q8 = N.cast_fp8(q_cols, 4.0).view(-1, B, H, hd).transpose(0, 1)
         k8 = N.cast_fp8(k_cols, 0.25).view(-1, B, H, hd).transpose(0, 1)
         kw = dict(attn_kw, fp8_qk=(q8, k8))
-        if self.attention_precision == "fp8":
+        if self.attention_precision == "fp8" and 1.13 * qb * kb <= 30.0:
             kw["fp8_v"] = N.cast_v_fp8t(v)
         return kw
 
     def _self_attn_mode(self, i: int, hd: int):
-        """(q out_scale, attn_fwd kwargs) of block i's self-attention. When the norm bound allows
-        (|q| |k| scale log2(e) <= 60, always for RMS-normed rows with |w| <= ~1.9), q leaves the
-        RMSNorm/RoPE kernel as bf16(q * hd^-0.5 * log2(e)) and the attention runs without its
-        per-score multiply (cp25_attn_fwd_prescaled, +4 % on the kernel). That rounds q * c instead of
-        q to bf16: the same single bf16 rounding of the query at the same relative size, so the
-        distance to the fp32 truth is unchanged (tests/test_parity_depth_gpu.py holds the HIP path
-        within 1.1x of the bf16 reference's own distance); `exact_q_rounding = True` keeps the
-        reference's rounding point (q rounded, scale applied to the fp32 scores)."""
+        """(q out_scale, attn_fwd kwargs) of block i's self-attention. q leaves the RMSNorm/RoPE kernel as
+        bf16(q * hd^-0.5 * log2(e)) and the attention runs without a per-score multiply (cp25_attn_fwd_prescaled):
+        the softmax shift rides in the Q K^T chains' initial C, fixed from the weight norm bounds where they allow
+        it (bound product <= 80 in log2 units, e.g. the unit init weights) and an online row max otherwise (trained
+        q/k norm weights of any size). Rounding q * c instead of q to bf16 is the same single bf16 rounding of the
+        query at the same relative size, so the distance to the fp32 truth is unchanged
+        (tests/test_parity_depth_gpu.py holds the HIP path within 1.1x of the bf16 reference's own distance);
+        `exact_q_rounding = True` keeps the reference's rounding point (q rounded, scale applied to the fp32
+        scores)."""
         return self._attn_mode(self.attn_bounds[i], hd)
 
     def _attn_mode(self, bounds, hd: int):
         """The rule of _self_attn_mode for any RMS-normed q / k pair (also the text cross-attention)."""
         qb, kb = bounds
         c = hd ** -0.5 * 1.4426950408889634
-        if not self.exact_q_rounding and qb * c * kb <= 60.0:
+        if not self.exact_q_rounding:
             return c, dict(norm_bounds=(qb * c, kb), prescaled=True)
         return 1.0, dict(softmax_scale=hd ** -0.5, norm_bounds=(qb, kb))
 
@@ -291,11 +292,34 @@ class MinimalV1LVGDiT:
             self._fp8_w[key] = ent
         return ent
 
-    def _mlp1_fused(self, x, w: torch.Tensor) -> bool:
-        """GPT2FeedForward layer1 + GELU (minimal_v4_dit.py:249-254) on cp25_gemm_epi's GELU epilogue: bf16 linears,
-        shapes the kernel is built for, and `mlp1_gemm == "own"` (CP25_MLP1_GEMM=own; the default "lib" keeps hipBLASLt + cp25_gelu)."""
-        return (self.mlp1_gemm == "own" and not isinstance(x, tuple) and self.linear_precision == "bf16"
+    def _own(self, x, w: torch.Tensor) -> bool:
+        """The hand-written GEMM runs this projection: bf16 linears, shapes it is built for, block_gemm == "own"."""
+        return (self.block_gemm == "own" and not isinstance(x, tuple) and self.linear_precision == "bf16"
                 and N.gemm_supported(w.shape[0], w.shape[1]))
+
+    def _proj(self, x, w: torch.Tensor, key: str) -> torch.Tensor:
+        """A block projection without epilogue (QKV, cross-attention q)."""
+        return N.gemm_epi(x, w) if self._own(x, w) else self._linear(x, w, key)
+
+    def _proj_res(self, a, w: torch.Tensor, key: str, x: torch.Tensor, x_st: int, x_sb: int, gate: torch.Tensor,
+                  B: int, geo: "Geometry", n: int, lnk: dict, shift=None, scale=None):
+        """x' = x + gate * (a w^T) (Block.forward's gated residuals, minimal_v4_dit.py:1204, 1237, 1246) for the token-
+        major [n, B, D] rows, then (if shift is given) h = LN-mod(x') for the next sub-layer. Own GEMM: the residual
+        rides in its epilogue (cp25_gemm_res) and the LN-mod reads x' only; else hipBLASLt + the residual in
+        cp25_ln_mod. Returns (x' [n, B, D], h or None)."""
+        D = w.shape[0]
+        if self._own(a, w):
+            x_new = N.gemm_res(a, w, x, x_st, x_sb, gate, B=B, tok0=geo.tok0, hw=geo.hw).view(n, B, D)
+            h = None
+            if shift is not None:
+                h = N.ln_mod(x_new, shift, scale, x_st=B * D, x_sb=D, **dict(lnk, B=B))
+            return x_new, h
+        if shift is None:
+            raise ValueError("the library-GEMM path fuses the last residual into the final layer instead")
+        y = self._linear(a, w, key)
+        x_new = torch.empty((n, B, D), dtype=BF16, device=self.device)
+        h = N.ln_mod(x, shift, scale, x_st=x_st, x_sb=x_sb, y=y, gate=gate, x_out=x_new, **dict(lnk, B=B))
+        return x_new, h
 
     def _linear(self, x, w: torch.Tensor, key: str, gelu_in: bool = False) -> torch.Tensor:
         """y = x w^T for a block projection (x [M, K] bf16 contiguous, or an fp8 operand pair (q, scale)
@@ -346,9 +370,17 @@ class MinimalV1LVGDiT:
         self.w_ada2 = torch.stack([p[f"blocks.{i}.adaln_modulation_{m}.2.weight"]
                                    for i in range(cfg.num_blocks) for m in ("self_attn", "cross_attn", "mlp")], 0).float()
         self.w_final = p["final_layer.linear.weight"].float()
-        # per-block (max|q|, max|k|) bounds for the bounded-shift attention softmax: the q/k RMSNorm
-        # (minimal_v4_dit.py:355-358) leaves every head row with |x| <= sqrt(hd) * max|weight|, RoPE
-        # is a rotation; 2 % covers the two bf16 roundings. One host read per weight, at load time.
+        self.refresh_norm_bounds()
+        self._rope_cache.clear()
+        if D % 512:
+            raise ValueError("model_channels must be a multiple of 512")
+
+    def refresh_norm_bounds(self) -> None:
+        """Per-block (max|q|, max|k|) bounds for the attention softmax shift: the q/k RMSNorm (minimal_v4_dit.py:355-358)
+        leaves every head row with |x| <= sqrt(hd) * max|weight|, RoPE is a rotation; 2 % covers the two bf16
+        roundings. One host read per weight, at load time (call again after changing a q/k norm weight). The
+        library picks the shift mode from them (a fixed shift where the product allows, else an online max)."""
+        cfg, p = self.cfg, self.sd
         hd = cfg.head_dim
 
         def nb(w: torch.Tensor) -> float:
@@ -358,9 +390,19 @@ class MinimalV1LVGDiT:
                             for i in range(cfg.num_blocks)]
         self.xattn_bounds = [(nb(p[f"blocks.{i}.cross_attn.q_norm.weight"]),
                               nb(p[f"blocks.{i}.cross_attn.k_norm.weight"])) for i in range(cfg.num_blocks)]
-        self._rope_cache.clear()
-        if D % 512:
-            raise ValueError("model_channels must be a multiple of 512")
+
+    def attention_kernels(self, L: int) -> Dict[str, str]:
+        """The attention kernel forms block 0 launches at L tokens (self) and against the text context (cross)."""
+        hd = self.cfg.head_dim
+        out = {}
+        for name, bounds, lk in (("self", self.attn_bounds[0], L), ("cross", self.xattn_bounds[0], 512)):
+            _, kw = self._attn_mode(bounds, hd)
+            fp8 = 0
+            if name == "self" and kw.get("prescaled") and self.attention_precision != "bf16":
+                qb, kb = kw["norm_bounds"]
+                fp8 = 0 if qb * kb > 60.0 else (2 if self.attention_precision == "fp8" and 1.13 * qb * kb <= 30.0 else 1)
+            out[name] = N.attn_kernel_name(lk, kw.get("softmax_scale"), kw["norm_bounds"], kw.get("prescaled", False), fp8)
+        return out
 
     def state_dict_keys(self) -> List[str]:
         return list(state_dict_shapes(self.cfg).keys())
@@ -621,7 +663,7 @@ class MinimalV1LVGDiT:
                 if self.attn_events is not None:
                     ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 if cp is None or cp_size == 1:
-                    qkv = self._linear(_rows(h, n * Bs), self.w_qkv[i], f"qkv.{i}")  # [n*Bs, 3D]
+                    qkv = self._proj(_rows(h, n * Bs), self.w_qkv[i], f"qkv.{i}")  # [n*Bs, 3D]
                     q_scale, attn_kw = self._self_attn_mode(i, hd)
                     N.head_rmsnorm_rope(qkv, n_rows=n * Bs, B=Bs, H=H, head_off=0,
                                         weight=p[pre + "self_attn.q_norm.weight"], cos=cos, sin=sin, out_scale=q_scale)
@@ -642,52 +684,55 @@ class MinimalV1LVGDiT:
                 if ev is not None:
                     ev[1].record()
                     self.attn_events.append((ev[0], ev[1], 4.0 * Bs * H * n * lk * hd))
-                y = self._linear(o.view(n * Bs, D), p[pre + "self_attn.output_proj.weight"], pre + "self_attn.output_proj")
-                # ---- x += g_sa * y ; LN-mod for cross attention
+                # ---- x += g_sa * (o W_o^T) ; LN-mod for cross attention
                 nb = 1 if Bs == 1 and B > 1 else None
                 _, _, g_sa = mod(i, 0, nb)
                 sh, sc, _ = mod(i, 1, nb)
-                x_new = torch.empty((n, Bs, D), dtype=BF16, device=self.device)
                 if i == 0:
                     x_st, x_sb = x_in.stride(0), (0 if Bx == 1 else x_in.stride(1))
                 else:
                     x_st, x_sb = B * D, D
-                h = N.ln_mod(x, sh, sc, x_st=x_st, x_sb=x_sb, y=y, gate=g_sa, x_out=x_new, **dict(lnk, B=Bs))
-                x = x_new
+                x, h = self._proj_res(o.view(n * Bs, D), p[pre + "self_attn.output_proj.weight"], pre + "self_attn.output_proj",
+                                      x, x_st, x_sb, g_sa, Bs, geo, n, lnk, sh, sc)
             if prefix_only:
                 return x, h
             # ---- cross attention (a shared query is read with batch stride 0 against each entry's text K/V)
-            qc = self._linear(_rows(h, n * Bs), p[pre + "cross_attn.q_proj.weight"], pre + "cross_attn.q_proj")
+            qc = self._proj(_rows(h, n * Bs), p[pre + "cross_attn.q_proj.weight"], pre + "cross_attn.q_proj")
             xq_scale, xattn_kw = self._attn_mode(self.xattn_bounds[i], hd)  # prescaled q as in self-attention
             N.head_rmsnorm_rope(qc, n_rows=n * Bs, B=Bs, H=H, head_off=0, weight=p[pre + "cross_attn.q_norm.weight"],
                                 out_scale=xq_scale)
             o = torch.empty((n, B, D), dtype=BF16, device=self.device)
             self._cross_attention(qc.view(n, Bs, H, hd).expand(n, B, H, hd), ctx.k[i], ctx.v[i], o.view(n, B, H, hd),
                                   geo, xattn_kw)
-            y = self._linear(o.view(n * B, D), p[pre + "cross_attn.output_proj.weight"], pre + "cross_attn.output_proj")
             _, _, g_ca = mod(i, 1)
             sh, sc, _ = mod(i, 2)
-            x_new = torch.empty((n, B, D), dtype=BF16, device=self.device)
-            h = N.ln_mod(x, sh, sc, x_st=Bs * D, x_sb=0 if Bs == 1 else D, y=y, gate=g_ca, x_out=x_new, **lnk)
-            x = x_new
+            x, h = self._proj_res(o.view(n * B, D), p[pre + "cross_attn.output_proj.weight"], pre + "cross_attn.output_proj",
+                                  x, Bs * D, 0 if Bs == 1 else D, g_ca, B, geo, n, lnk, sh, sc)
             # ---- MLP
             h1 = _rows(h, n * B)
-            w1 = p[pre + "mlp.layer1.weight"]
-            if self._mlp1_fused(h1, w1):
-                # layer1 + exact-erf GELU in one hand-written MFMA GEMM (the epilogue applies it to the bf16
-                # product, as cp25_gelu would): the [n B, 4 D] hidden makes one HBM trip instead of three
+            w1, w2 = p[pre + "mlp.layer1.weight"], p[pre + "mlp.layer2.weight"]
+            _, _, g_ml = mod(i, 2)
+            last = i + 1 == cfg.num_blocks
+            sh, sc = (None, None) if last else mod(i + 1, 0)[:2]
+            if self._own(h1, w1):
+                # layer1 + exact-erf GELU in one hand-written MFMA GEMM (the epilogue applies it to the bf16 product, as
+                # cp25_gelu would): the [n B, 4 D] hidden makes one HBM trip instead of three
                 u = N.gemm_epi(h1, w1, epilogue=N.EPI_GELU)
-                y = self._linear(u, p[pre + "mlp.layer2.weight"], pre + "mlp.layer2")
             else:
                 u = self._linear(h1, w1, pre + "mlp.layer1")
-                y = self._linear(u, p[pre + "mlp.layer2.weight"], pre + "mlp.layer2", gelu_in=True)
+                if self.linear_precision == "bf16":
+                    N.gelu_(u)
+            if self._own(u, w2):
+                x, h = self._proj_res(u, w2, pre + "mlp.layer2", x, B * D, D, g_ml, B, geo, n, lnk, sh, sc)
+                y, gate_prev = None, None
+            else:
+                y = self._linear(u, w2, pre + "mlp.layer2", gelu_in=self.linear_precision != "bf16")
+                gate_prev = g_ml
+                if not last:
+                    x_new = torch.empty((n, B, D), dtype=BF16, device=self.device)
+                    h = N.ln_mod(x, sh, sc, x_st=B * D, x_sb=D, y=y, gate=gate_prev, x_out=x_new, **lnk)
+                    x = x_new
             del u
-            _, _, gate_prev = mod(i, 2)
-            if i + 1 < cfg.num_blocks:
-                sh, sc, _ = mod(i + 1, 0)
-                x_new = torch.empty((n, B, D), dtype=BF16, device=self.device)
-                h = N.ln_mod(x, sh, sc, x_st=B * D, x_sb=D, y=y, gate=gate_prev, x_out=x_new, **lnk)
-                x = x_new
             if cp is None or cp_size == 1:
                 yield i
         # ---- final layer (fp32 autocast): x + g*y -> LN -> modulate -> Linear(D -> 64)
@@ -725,7 +770,7 @@ class MinimalV1LVGDiT:
         p = self.sd
         pre = f"blocks.{i}."
         D, H, hd = cfg.model_channels, cfg.num_heads, cfg.head_dim
-        qkv = self._linear(_rows(h, n * B), self.w_qkv[i], f"qkv.{i}")  # [n*B, 3D]
+        qkv = self._proj(_rows(h, n * B), self.w_qkv[i], f"qkv.{i}")  # [n*B, 3D]
         N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=D, weight=p[pre + "self_attn.k_norm.weight"],
                             cos=cos, sin=sin)
         kv = torch.empty((n * B, 2 * D), dtype=BF16, device=self.device)

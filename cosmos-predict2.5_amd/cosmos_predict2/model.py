@@ -253,11 +253,15 @@ class SamplingRun:
         self.action, self.view_indices = action, view_indices
         self._sched_args = dict(num_inference_steps=num_steps, device=dev, shift=shift,
                                 use_kerras_sigma=model.config.use_kerras_sigma_at_inference)
+        # the run's own solver (configured like the model's sample_scheduler): its UniPC history must not be shared
+        # with another live run, nor with a sample_latents call made while this run is alive
+        base = model.sample_scheduler
+        self.sched = FlowUniPCMultistepScheduler(base.num_train_timesteps, base.solver_order, base.config_shift)
         self.restart()
 
     def restart(self) -> None:
         """Back to the first timestep from the same noise (bench: more evaluations than one trajectory)."""
-        sched = self.model.sample_scheduler
+        sched = self.sched
         sched.set_timesteps(**self._sched_args)
         self.timesteps = sched.timesteps.cpu()
         self.x = sched.begin(self.noise)
@@ -291,7 +295,7 @@ class SamplingRun:
         v = N.cfg_velocity(net_out, self.noise, self.gtp, self.frame_mask, self.guidance, self.mode,
                            tok0=geo.tok0, hw=geo.hw)
         del net_out
-        m.sample_scheduler.step_(v, t)
+        self.sched.step_(v, t)
         self.i += 1
         return self.i - 1
 

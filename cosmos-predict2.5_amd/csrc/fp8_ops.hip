@@ -237,64 +237,7 @@ __global__ void __launch_bounds__(256) v_cast_t_kernel(const unsigned short* __r
   }
 }
 
-// ---- bf16 V^T for the 16x16x32 self-attention (cp25_attn_fwd_prescaled_vt): the O^T = V^T P^T MFMA's A operand,
-// lane (c, g) of key step ks holds V[key][16 db + c] for the 8 keys 32 ks + 16 (j >> 2) + 4 g + (j & 3), j < 8 (the
-// order the P^T operand packs them from the S^T accumulator). A V^T row d of a 64-key tile is stored as 64 bf16 at
-// p = 32 ks + 8 g + j, so the fragment is one contiguous 16-B read (one ds_read_b128 instead of two transposed
-// ds_read_b64_tr_b16): vt[b][h][tile][d][p]. Keys past L are zero. Exact copy (no rounding).
-__device__ __forceinline__ int vt16_key(int p) {
-  const int ks = p >> 5, g = (p >> 3) & 3, j = p & 7;
-  return 32 * ks + 16 * (j >> 2) + 4 * g + (j & 3);
-}
-
-// one tile (b, h, tile): 64 keys x 128 d through LDS, out as [128 d][64 p] bf16. grid (B * H, ntile), 256 threads.
-__global__ void __launch_bounds__(256) v_t16_kernel(const unsigned short* __restrict__ v, int64_t sb, int64_t sl,
-                                                    int64_t sh, int H, int L, int ntile,
-                                                    unsigned short* __restrict__ vt) {
-  constexpr int RS = 128 + 8;  // LDS row stride (bf16 elements; 16-B aligned rows for the vector stores)
-  __shared__ __attribute__((aligned(16))) unsigned short t[64 * RS];
-  const int bh = blockIdx.x, b = bh / H, h = bh % H, tile = blockIdx.y;
-  const unsigned short* vp = v + b * sb + h * sh;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {  // 1024 chunks of 8 bf16: key c / 16, d 8 (c % 16)
-    const int c = threadIdx.x + 256 * i, key = c >> 4, d0 = 8 * (c & 15), row = 64 * tile + key;
-    u32x4 w = {0u, 0u, 0u, 0u};
-    if (row < L) w = *reinterpret_cast<const u32x4*>(vp + (int64_t)row * sl + d0);
-    *reinterpret_cast<u32x4*>(t + key * RS + d0) = w;
-  }
-  __syncthreads();
-  unsigned short* out = vt + ((int64_t)bh * ntile + tile) * 8192;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {  // 1024 output chunks of 8 bf16: d = c / 8, p0 = 8 (c % 8)
-    const int c = threadIdx.x + 256 * i, d = c >> 3, p0 = 8 * (c & 7);
-    u32x4 o;
-#pragma unroll
-    for (int w = 0; w < 4; ++w)
-      o[w] = (unsigned)t[vt16_key(p0 + 2 * w) * RS + d] | ((unsigned)t[vt16_key(p0 + 2 * w + 1) * RS + d] << 16);
-    *reinterpret_cast<u32x4*>(out + d * 64 + p0) = o;
-  }
-}
-
 }  // namespace
-
-extern "C" int64_t cp25_v_bf16t_bytes(int B, int H, int L) {
-  if (B <= 0 || H <= 0 || L <= 0) return CP25_ERR_INVAL;
-  return (int64_t)B * H * cdiv(L, 64) * 16384;
-}
-
-extern "C" int cp25_cast_v_bf16t(const void* v, const int64_t* v_strides, int B, int H, int L, int D, void* vt,
-                                 hipStream_t stream) {
-  if (!v || !v_strides || !vt || B <= 0 || H <= 0 || L <= 0) return CP25_ERR_INVAL;
-  if (D != 128) return CP25_ERR_DTYPE;
-  for (int j = 0; j < 3; ++j)
-    if (v_strides[j] % 8) return CP25_ERR_INVAL;
-  if ((((uintptr_t)v) | ((uintptr_t)vt)) & 15) return CP25_ERR_INVAL;
-  const int ntile = (int)cdiv(L, 64);
-  hipLaunchKernelGGL(v_t16_kernel, dim3(B * H, ntile), dim3(256), 0, stream, (const unsigned short*)v, v_strides[0],
-                     v_strides[1], v_strides[2], H, L, ntile, (unsigned short*)vt);
-  CP25_LAUNCH_CHECK();
-  return CP25_OK;
-}
 
 extern "C" int64_t cp25_v_fp8t_bytes(int B, int H, int L) {
   if (B <= 0 || H <= 0 || L <= 0) return CP25_ERR_INVAL;

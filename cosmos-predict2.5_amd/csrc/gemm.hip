@@ -9,6 +9,12 @@
 //                                     output (:249-254: `x = self.layer1(x); x = self.activation(x)`),
 //                                     the same arithmetic as cp25_gelu, so the MLP hidden never makes
 //                                     the separate 2 x 3.6 GB GELU round trip.
+//                     CP25_EPI_RES  : C = bf16(x + bf16(gate * bf16(acc))), the block's gated residual
+//                                     (Block.forward :1204, :1237, :1246: x = x + gate * sublayer(x)) on the
+//                                     output / cross-output / layer2 projections, with x and gate read by the
+//                                     token-major row (tok, b) = (row / B, row % B) and the row's frame
+//                                     (tok0 + tok) / hw; the next LN-mod then reads the new x once instead of x
+//                                     and y (cp25_ln_mod with y = NULL).
 //
 // Design (MI355X, see DESIGN.md §3 "GEMM"): 256 x 256 output tile per 512-thread workgroup (one per
 // CU), 8 waves as 2 (M) x 4 (N), each wave 128 x 64 with v_mfma_f32_16x16x32_bf16 (32 accumulators,
@@ -20,13 +26,12 @@
 // their A and W tiles through that XCD's L2.
 //   * gemm_nt_8ph (default, K/64 even): persistent, 8-phase schedule with counted vmcnt across raw barriers
 //     and a pipelined tile seam (below).
-//   * gemm_nt_kernel (odd K/64, or CP25_GEMM_KERNEL=2ph): the round-2 two-phase loop (vmcnt(0) +
-//     __syncthreads per K-tile), one workgroup per tile. Both accumulate in the same order: bit-identical.
+//   * gemm_nt_kernel (odd K/64): the round-2 two-phase loop (vmcnt(0) + __syncthreads per K-tile), one workgroup
+//     per tile. Both accumulate in the same order: bit-identical. Every output row is computed the same way
+//     whatever M is (no split-K, fixed K order), so a context-parallel shard's rows equal the full run's bit for bit.
 #include "cp25_common.h"
 
 #include <algorithm>
-#include <cstdlib>
-#include <cstring>
 #include <type_traits>
 
 #pragma clang fp contract(off)
@@ -50,10 +55,36 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, lds_void_ptr 
 
 __device__ __forceinline__ float gelu_exact(float a) { return gelu_erf(a); }  // = cp25_gelu (cp25_common.h)
 
+// CP25_EPI_RES operands: output row r = token (r / B) batch entry (r % B); x element (tok, b, col) at
+// tok * x_st + b * x_sb + col, gate element (b, frame, col) at b * g_sb + frame * g_st + col, frame = (tok0 + tok) / hw
+struct ResEpi {
+  const unsigned short* x; int64_t x_st, x_sb;
+  const unsigned short* gate; int64_t g_sb, g_st;
+  int B; int64_t tok0, hw;
+};
+
+// x + gate * y on 8 bf16 columns, two bf16 roundings (the reference's two torch ops, = cp25_ln_mod's residual)
+__device__ __forceinline__ u32x4 res8(u32x4 y, u32x4 x, u32x4 g) {
+  u32x4 o;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    unsigned r = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float yv = bf2f((unsigned short)(y[w] >> (16 * h)));
+      const float xv = bf2f((unsigned short)(x[w] >> (16 * h)));
+      const float gv = bf2f((unsigned short)(g[w] >> (16 * h)));
+      r |= (unsigned)f2bf(rbf(xv + rbf(gv * yv))) << (16 * h);
+    }
+    o[w] = r;
+  }
+  return o;
+}
+
 template <int kEpi>
 __global__ void __launch_bounds__(kThreads, 1)
 gemm_nt_kernel(const unsigned short* __restrict__ A, int64_t lda, const unsigned short* __restrict__ W, int64_t ldw,
-               unsigned short* __restrict__ C, int64_t ldc, int M, int N, int K) {
+               unsigned short* __restrict__ C, int64_t ldc, int M, int N, int K, ResEpi re) {
   __shared__ __attribute__((aligned(16))) char smem[kLds];
 
   const int mt = (M + kBM - 1) / kBM, nt = N / kBN;
@@ -155,9 +186,17 @@ gemm_nt_kernel(const unsigned short* __restrict__ A, int64_t lda, const unsigned
   for (int it = 0; it < 16; ++it) {
     const int idx = it * 64 + lane;  // 128 rows x 8 chunks of 16 B
     const int r = idx >> 3, ch = idx & 7;
-    if (row0 + r < M)
-      *reinterpret_cast<u32x4*>(C + (int64_t)(row0 + r) * ldc + col0 + ch * 8) =
-          *reinterpret_cast<const u32x4*>(st + r * 64 + ch * 8);
+    if (row0 + r < M) {
+      u32x4 v = *reinterpret_cast<const u32x4*>(st + r * 64 + ch * 8);
+      if constexpr (kEpi == CP25_EPI_RES) {
+        const int row = row0 + r, tok = row / re.B, b = row % re.B;
+        const int64_t fr = (re.tok0 + tok) / re.hw;
+        const u32x4 xv = *reinterpret_cast<const u32x4*>(re.x + tok * re.x_st + b * re.x_sb + col0 + ch * 8);
+        const u32x4 gv = *reinterpret_cast<const u32x4*>(re.gate + b * re.g_sb + fr * re.g_st + col0 + ch * 8);
+        v = res8(v, xv, gv);
+      }
+      *reinterpret_cast<u32x4*>(C + (int64_t)(row0 + r) * ldc + col0 + ch * 8) = v;
+    }
   }
 }
 
@@ -187,13 +226,15 @@ constexpr int kBuf8 = 4 * kHalf;      // A0 A1 B0 B1
 // vmcnt(6 + 16) at phase 3 of K-tile 0 retires K-tile 1; by phase 3 of K-tile 1 the stores have had two K-tiles
 // to drain. (Issued in the epilogue with a plain vmcnt(0) wait they cost 8-12 % at K = 2048.) A ragged last
 // row-tile masks its stores, so the counts there fall back to vmcnt(0).
-// kLab (A/B only, CP25_GEMM_KERNEL=8ph_lab<n>): bit 0 skips the C staging and stores (accumulators kept live),
-// bit 4 stages C but skips the global stores, bit 6 makes the C stores nontemporal
-// (measured: a CU start stagger and nontemporal stores do not help at K >= 2048; see DESIGN.md §3 "GEMM").
-template <int kEpi, int kLab = 0>
+// CP25_EPI_RES: this thread's 16 x / gate chunks are loaded at the tile's end, once the accumulators are in the LDS
+// (the VM queue is empty there: the last K-tile's phase 3 retired everything), land while C is read back, and are
+// combined before the stores.
+// (Round-2 A/B variants of this kernel -- skipped / nontemporal stores, the lab switches -- are in git history,
+// DESIGN.md §3 "GEMM".)
+template <int kEpi>
 __global__ void __launch_bounds__(kThreads, 1)
 gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned short* __restrict__ W, int64_t ldw,
-            unsigned short* __restrict__ C, int64_t ldc, int M, int N, int K) {
+            unsigned short* __restrict__ C, int64_t ldc, int M, int N, int K, ResEpi re) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kBuf8];
 
   const int mt = (M + kBM - 1) / kBM, nt = N / kBN;
@@ -362,25 +403,6 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
 
     const int next = tile + gridDim.x;
     const bool has_next = next < n_tiles;
-    if constexpr (kLab & 1) {
-#pragma unroll
-      for (int mq = 0; mq < 2; ++mq)
-#pragma unroll
-        for (int nq = 0; nq < 2; ++nq)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(acc[mq][nq][i][j]));
-      if (!has_next) return;
-      tile = next;
-      tile_mn(tile, m0, n0);
-      set_tile(m0, n0);
-      issue_first_two();
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      continue;
-    }
-
     // ---- C tile -> LDS [256][256] bf16 (row stride 512 B; 16-B chunk ch of row r at ch ^ sw(r), sw(r) =
     // 2 ((r >> 2) & 3) = 2 fg for this wave's rows, so the four row groups of a fragment write hit distinct banks).
     // Element (row, col): row = mq 128 + wr 64 + 16 i + 4 fg + r, col = nq 128 + wc 32 + 16 j + fr; the lane part
@@ -408,16 +430,46 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
               if constexpr (kEpi == CP25_EPI_GELU) y = gelu_exact(y);
               stj[j][(mq * 128 + 16 * i + r) * 256 + nq * 128] = f2bf(y);
             }
+    // (after the accumulators are in the LDS: their registers hold the x / gate chunks)
+    // thread t owns rows m0 + 16 it + t / 32 (it = 0..15), 16-B chunk t % 32 of the C tile
+    const int ch = tid & 31, r0 = tid >> 5;
+    u32x4 xres[16], gres[16];
+    if constexpr (kEpi == CP25_EPI_RES) {
+      // row r0 + 16 it: token tok_a + it * (16 / B), batch entry b (16 % B == 0), frame by a running remainder that
+      // wraps at most once per step (16 / B <= hw, host-checked): straight-line code. Rows past M (a ragged last
+      // row-tile) read the thread's first valid row instead (their results are not stored).
+      const int row_a = min(m0 + r0, M - 1), tok_a = row_a / re.B, b = row_a % re.B, dtok = 16 / re.B;
+      int64_t fr = (re.tok0 + tok_a) / re.hw, rem = (re.tok0 + tok_a) % re.hw;
+      const unsigned short* xp = re.x + (int64_t)tok_a * re.x_st + b * re.x_sb + n0 + ch * 8;
+      const unsigned short* gp = re.gate + b * re.g_sb + n0 + ch * 8;
+      const int n_valid = (M - 1 - row_a) / 16;  // rows row_a + 16 it, it <= n_valid, exist
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const bool ok = it <= n_valid;
+        xres[it] = *reinterpret_cast<const u32x4*>(ok ? xp + (int64_t)it * dtok * re.x_st : xp);
+        gres[it] = *reinterpret_cast<const u32x4*>(ok ? gp + fr * re.g_st : gp);
+        rem += dtok;
+        const bool wrap = rem >= re.hw;
+        rem -= wrap ? re.hw : 0;
+        fr += wrap ? 1 : 0;
+      }
+    }
+
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     // thread t reads rows 16 it + t / 32 (it = 0..15), 16-B chunk t % 32 (sw(row) depends on t only)
-    const int ch = tid & 31, r0 = tid >> 5;
     const unsigned short* rd = ct + ez + r0 * 256 + ((ch ^ (((r0 >> 2) & 3) << 1)) << 3);
     u32x4 cv[16];
 #pragma unroll
     for (int it = 0; it < 16; ++it) cv[it] = *reinterpret_cast<const u32x4*>(rd + it * 16 * 256);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // the LDS is free for the next tile's DMA
+    if constexpr (kEpi == CP25_EPI_RES) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the x / gate chunks (nothing else is in flight)
+#pragma unroll
+      for (int it = 0; it < 16; ++it)
+        if (m0 + r0 + 16 * it < M) cv[it] = res8(cv[it], xres[it], gres[it]);
+    }
 
     unsigned short* crow = C + (int64_t)(m0 + r0) * ldc + n0 + ch * 8;
     const bool full = m0 + kBM <= M;
@@ -429,28 +481,17 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
       issue_first_two();
     }
     __builtin_amdgcn_sched_barrier(0);  // the DMAs are queued ahead of the stores (the counts above rely on it)
-    if constexpr (!(kLab & 16)) {
-      if (full) {
-        if constexpr ((kLab & 64) != 0) {
+    if (full) {
 #pragma unroll
-          for (int it = 0; it < 16; ++it)
-            __builtin_nontemporal_store(cv[it], reinterpret_cast<u32x4*>(crow + (int64_t)it * 16 * ldc));
-        } else {
-#pragma unroll
-          for (int it = 0; it < 16; ++it) *reinterpret_cast<u32x4*>(crow + (int64_t)it * 16 * ldc) = cv[it];
-        }
-      } else {
-#pragma unroll
-        for (int it = 0; it < 16; ++it)
-          if (it * 16 < rows_left) *reinterpret_cast<u32x4*>(crow + (int64_t)it * 16 * ldc) = cv[it];
-      }
+      for (int it = 0; it < 16; ++it) *reinterpret_cast<u32x4*>(crow + (int64_t)it * 16 * ldc) = cv[it];
     } else {
 #pragma unroll
-      for (int it = 0; it < 16; ++it) asm volatile("" ::"v"(cv[it]));
+      for (int it = 0; it < 16; ++it)
+        if (it * 16 < rows_left) *reinterpret_cast<u32x4*>(crow + (int64_t)it * 16 * ldc) = cv[it];
     }
     if (!has_next) return;
     // retire the next tile's K-tile 0: the stores (16, when all issued) and K-tile 1 (8) may stay in flight
-    stores_pending = full && !(kLab & 16);
+    stores_pending = full;
     if (stores_pending)
       asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
     else
@@ -460,22 +501,25 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
 }
 }  // namespace
 
-extern "C" int cp25_gemm_epi(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int M,
-                             int N, int K, int epilogue, hipStream_t stream) {
+static int gemm_launch(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int M, int N,
+                       int K, int epilogue, const ResEpi& re, hipStream_t stream) {
   if (!a || !w || !c || M <= 0 || N <= 0 || K <= 0) return CP25_ERR_INVAL;
   if (N % kBN != 0 || K % kBK != 0) return CP25_ERR_DTYPE;  // the tiles this kernel is built for
   if (lda < K || ldw < K || ldc < N || (lda % 8) || (ldw % 8) || (ldc % 8)) return CP25_ERR_INVAL;
   if (lda >= (1 << 22) || ldw >= (1 << 22)) return CP25_ERR_INVAL;  // 32-bit in-tile byte offsets
   if (((uintptr_t)a | (uintptr_t)w | (uintptr_t)c) & 15) return CP25_ERR_INVAL;
+  if (epilogue != CP25_EPI_NONE && epilogue != CP25_EPI_GELU && epilogue != CP25_EPI_RES) return CP25_ERR_INVAL;
+  if (epilogue == CP25_EPI_RES) {
+    if (!re.x || !re.gate || re.B <= 0 || 16 % re.B || re.hw < 16 / re.B || re.tok0 < 0 || (re.x_st % 8) || (re.x_sb % 8) ||
+        (re.g_sb % 8) || (re.g_st % 8) || (((uintptr_t)re.x | (uintptr_t)re.gate) & 15))
+      return CP25_ERR_INVAL;
+    if ((int64_t)(M - 1) / re.B * re.x_st >= (1ll << 40)) return CP25_ERR_INVAL;
+  }
   const int64_t nwg = (int64_t)((M + kBM - 1) / kBM) * (N / kBN);
   if (nwg > 0x7fffffff) return CP25_ERR_INVAL;
   const unsigned short* A = (const unsigned short*)a;
   const unsigned short* Wp = (const unsigned short*)w;
   unsigned short* Cp = (unsigned short*)c;
-  if (epilogue != CP25_EPI_NONE && epilogue != CP25_EPI_GELU) return CP25_ERR_INVAL;
-  const char* sel = std::getenv("CP25_GEMM_KERNEL");  // "2ph": the round-2 two-phase loop (A/B only)
-  const bool two_phase = sel && !std::strcmp(sel, "2ph");
-  const bool gelu = epilogue == CP25_EPI_GELU;
   const dim3 grid((unsigned)nwg), block(kThreads);
   static int n_cu[64] = {0};
   int dev = 0;
@@ -484,28 +528,43 @@ extern "C" int cp25_gemm_epi(const void* a, int64_t lda, const void* w, int64_t 
     return CP25_ERR_LAUNCH;
   const int cus = n_cu[dev] >= 8 ? n_cu[dev] & ~7 : n_cu[dev];
   const dim3 pgrid((unsigned)std::min<int64_t>(nwg, cus));
-  const int lab = sel && !std::strncmp(sel, "8ph_lab", 7) ? std::atoi(sel + 7) : -1;
-  if (lab >= 0 && !gelu && (K / kBK) % 2 == 0) {
-#define CP25_LAB(n)                                                                                            \
-  case n:                                                                                                        \
-    hipLaunchKernelGGL((gemm_nt_8ph<CP25_EPI_NONE, n>), pgrid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K); \
-    break;
-    switch (lab) {
-      CP25_LAB(1) CP25_LAB(16) CP25_LAB(64)
-      default: return CP25_ERR_INVAL;
+  if ((K / kBK) % 2 != 0) {
+    switch (epilogue) {
+      case CP25_EPI_GELU:
+        hipLaunchKernelGGL(gemm_nt_kernel<CP25_EPI_GELU>, grid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re);
+        break;
+      case CP25_EPI_RES:
+        hipLaunchKernelGGL(gemm_nt_kernel<CP25_EPI_RES>, grid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re);
+        break;
+      default:
+        hipLaunchKernelGGL(gemm_nt_kernel<CP25_EPI_NONE>, grid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re);
     }
-#undef CP25_LAB
-  } else if (two_phase || (K / kBK) % 2 != 0) {
-    if (gelu)
-      hipLaunchKernelGGL(gemm_nt_kernel<CP25_EPI_GELU>, grid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K);
-    else
-      hipLaunchKernelGGL(gemm_nt_kernel<CP25_EPI_NONE>, grid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K);
   } else {
-    if (gelu)
-      hipLaunchKernelGGL((gemm_nt_8ph<CP25_EPI_GELU, 0>), pgrid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K);
-    else
-      hipLaunchKernelGGL((gemm_nt_8ph<CP25_EPI_NONE, 0>), pgrid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K);
+    switch (epilogue) {
+      case CP25_EPI_GELU:
+        hipLaunchKernelGGL(gemm_nt_8ph<CP25_EPI_GELU>, pgrid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re);
+        break;
+      case CP25_EPI_RES:
+        hipLaunchKernelGGL(gemm_nt_8ph<CP25_EPI_RES>, pgrid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re);
+        break;
+      default:
+        hipLaunchKernelGGL(gemm_nt_8ph<CP25_EPI_NONE>, pgrid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re);
+    }
   }
   CP25_LAUNCH_CHECK();
   return CP25_OK;
+}
+
+extern "C" int cp25_gemm_epi(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int M,
+                             int N, int K, int epilogue, hipStream_t stream) {
+  if (epilogue == CP25_EPI_RES) return CP25_ERR_INVAL;  // needs its operands: cp25_gemm_res
+  const ResEpi re{};
+  return gemm_launch(a, lda, w, ldw, c, ldc, M, N, K, epilogue, re, stream);
+}
+
+extern "C" int cp25_gemm_res(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int M,
+                             int N, int K, const void* x, int64_t x_st, int64_t x_sb, const void* gate, int64_t g_sb,
+                             int64_t g_st, int B, int64_t tok0, int64_t hw, hipStream_t stream) {
+  const ResEpi re{(const unsigned short*)x, x_st, x_sb, (const unsigned short*)gate, g_sb, g_st, B, tok0, hw};
+  return gemm_launch(a, lda, w, ldw, c, ldc, M, N, K, CP25_EPI_RES, re, stream);
 }

@@ -50,26 +50,26 @@ int cp25_attn_fwd_split(const void* q, const void* k, const void* v, void* o, in
                         size_t ws_bytes, hipStream_t stream);
 
 /* cp25_attn_fwd_split with caller-supplied upper bounds of the query and key norms:
- * q_norm_bound >= max |q| and k_norm_bound >= max |k| over all rows (0 = unknown). When both are given
- * and b = q_norm_bound * k_norm_bound * softmax_scale * log2(e) <= 80, every score of a row lies in
- * [-b_row, b_row] (Cauchy-Schwarz, b_row from the row's own |q|), so the row uses the fixed softmax
- * shift max(b_row - 60, 0) (softmax is shift invariant) instead of a running row max: no max
- * reduction and no output rescale per key tile. Every term stays within [2^-100, 2^60], inside the
- * fp32/bf16 range. Otherwise (or with a 0
- * bound) this is cp25_attn_fwd_split. Same result as cp25_attn_fwd_split up to rounding. The DiT
- * passes sqrt(D) * max|q_norm.weight| and sqrt(D) * max|k_norm.weight|: the q/k RMSNorm
- * (minimal_v4_dit.py:355-358) bounds every normed row by them and RoPE preserves the norm. */
+ * q_norm_bound >= max |q| and k_norm_bound >= max |k| over all rows (0 = unknown). Softmax is shift invariant, so a
+ * row's shift only has to keep its terms inside the fp32 / bf16 range. When both bounds are given and
+ * b = q_norm_bound * k_norm_bound * softmax_scale * log2(e) <= 80, every score of a row lies in [-b_row, b_row]
+ * (Cauchy-Schwarz, b_row from the row's own |q|) and the row uses the fixed shift max(b_row - 60, 0): no max
+ * reduction and no output rescale per key tile, every term within [2^-100, 2^60]. Otherwise (or with a 0 bound) the
+ * rows run an online max (tile 0 sets the shift to the row max; later tiles move it up, rescaling O and the sum, only
+ * when a row max exceeds it by more than 8): any data. Same result as cp25_attn_fwd_split up to rounding. The DiT
+ * passes sqrt(D) * max|q_norm.weight| and sqrt(D) * max|k_norm.weight|: the q/k RMSNorm (minimal_v4_dit.py:355-358)
+ * bounds every normed row by them and RoPE preserves the norm. */
 int cp25_attn_fwd_bounded(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq, int Lk,
                           int D, const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
                           const int64_t* o_strides, float softmax_scale, float q_norm_bound, float k_norm_bound,
                           int n_split, void* workspace, size_t ws_bytes, hipStream_t stream);
 
-/* Bounded-shift attention over a PRE-SCALED q (rows already multiplied by softmax_scale * log2(e), e.g.
- * by cp25_head_rmsnorm_rope_scaled): P = exp2(q k^T) with no per-score multiply and no shift. Requires
- * q_norm_bound * k_norm_bound <= 60 (bounds of |q_row| as scaled and of |k_row|), which keeps every
- * term in [2^-60, 2^60]; CP25_ERR_INVAL otherwise (the caller then runs cp25_attn_fwd_bounded on an
- * unscaled q). Rounds q * scale to bf16 instead of q: the config-5 fp8 option's attention.
- * Replaces the same reference code as cp25_attn_fwd_bounded. */
+/* cp25_attn_fwd_bounded over a PRE-SCALED q (rows already multiplied by softmax_scale * log2(e), e.g. by
+ * cp25_head_rmsnorm_rope_scaled): P = exp2(q k^T - shift) with the row's shift as the initial accumulator of its
+ * Q K^T MFMA chains, so no per-score multiply or subtract. Bounds (of the scaled q and of k; 0 = unknown) pick the
+ * shift as in cp25_attn_fwd_bounded: product <= 60 no shift, <= 80 a fixed per-row shift, else the online max.
+ * Rounds q * scale to bf16 instead of q (the same single bf16 rounding of the query). Replaces the same reference
+ * code as cp25_attn_fwd_bounded; the DiT's default form. */
 int cp25_attn_fwd_prescaled(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq, int Lk, int D,
                             const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
                             const int64_t* o_strides, float q_norm_bound, float k_norm_bound, int n_split,
@@ -80,7 +80,8 @@ int cp25_attn_fwd_prescaled(const void* q, const void* k, const void* v, void* o
 int cp25_cast_fp8_e4m3(const void* src, int64_t src_stride, void* dst, int64_t dst_stride, int64_t n_rows,
                        int64_t width, float scale, hipStream_t stream);
 
-/* The config-5 fp8 option's attention: cp25_attn_fwd_prescaled with q and k given as OCP e4m3 (one byte per
+/* The config-5 fp8 option's attention: cp25_attn_fwd_prescaled (zero shift: bound product <= 60) with q and k given
+ * as OCP e4m3 (one byte per
  * element; strides in elements = bytes, multiples of 16): q8 = e4m3(q * softmax_scale * log2(e) * 2^s),
  * k8 = e4m3(k * 2^-s) (cp25_cast_fp8_e4m3; the power-of-two scales cancel in q k^T, so no per-score multiply
  * returns). Q K^T runs on v_mfma_f32_32x32x64_f8f6f4; P and V stay bf16, o is bf16. The bounds are those of
@@ -90,21 +91,6 @@ int cp25_attn_fwd_prescaled_fp8qk(const void* q8, const void* k8, const void* v,
                                   int D, const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
                                   const int64_t* o_strides, float q_norm_bound, float k_norm_bound, int n_split,
                                   void* workspace, size_t ws_bytes, hipStream_t stream);
-
-/* bf16 V^T tiles for cp25_attn_fwd_prescaled_vt: vt[b][h][tile][128 d][64 p] with p = 32 ks + 8 g + j holding
- * V[32 ks + 16 (j >> 2) + 4 g + (j & 3)][d] (the key order of the 16x16x32 P^T operand), keys past L zero; an exact
- * copy of v ([B, L, H, 128] by element strides, 16-B aligned rows). cp25_v_bf16t_bytes gives the vt size.
- * Replaces: nothing in the reference (a layout of the V operand of networks/attention.py:90-181's softmax(QK^T)V). */
-int64_t cp25_v_bf16t_bytes(int B, int H, int L);
-int cp25_cast_v_bf16t(const void* v, const int64_t* v_strides, int B, int H, int L, int D, void* vt, hipStream_t stream);
-
-/* cp25_attn_fwd_prescaled with V given as cp25_cast_v_bf16t's vt instead of [B, L, H, 128] strides: the P.V operand
- * is one ds_read_b128 per fragment instead of two transposed reads (16x16x32 kernel only); bit-identical output.
- * Replaces: networks/attention.py:90-181 (attention(q, k, v)) as cp25_attn_fwd_prescaled does. */
-int cp25_attn_fwd_prescaled_vt(const void* q, const void* k, const void* vt, void* o, int B, int H, int Lq, int Lk,
-                               int D, const int64_t* q_strides, const int64_t* k_strides, const int64_t* o_strides,
-                               float q_norm_bound, float k_norm_bound, int n_split, void* workspace, size_t ws_bytes,
-                               hipStream_t stream);
 
 /* V for the fp8 P.V of cp25_attn_fwd_prescaled_fp8: v_amax[b * H + h] = max |v| over the head's L rows (float,
  * device memory, B * H entries), then v8t = e4m3(v * 448 / amax) laid out [B][H][ceil(L / 64)][128 d][64 key
@@ -116,14 +102,22 @@ int cp25_cast_v_fp8t(const void* v, const int64_t* v_strides, int B, int H, int 
                      hipStream_t stream);
 
 /* The config-5 fp8 option's whole attention: cp25_attn_fwd_prescaled_fp8qk's e4m3 Q K^T, then O^T += V^T P^T on
- * v_mfma_f32_32x32x64_f8f6f4 with P = exp2(S - shift) as e5m2 (shift = max(0, q_norm_bound * k_norm_bound - 15)
+ * v_mfma_f32_32x32x64_f8f6f4 with P = exp2(S - shift) as e5m2 (shift = max(0, 1.13 q_norm_bound k_norm_bound - 15)
  * keeps every P <= 2^15, inside e5m2, whatever the data) and V^T from cp25_cast_v_fp8t's v8t (O rescaled by
- * amax / 448 at the end). The softmax stays fp32 with no per-score multiply and no running max. o bf16. No
- * reference counterpart; replaces the same attention call. */
+ * amax / 448 at the end). The softmax stays fp32 with no per-score multiply and no running max. Requires
+ * 1.13 q_norm_bound k_norm_bound <= 30 (the window [2^-15, 2^15] then holds a term of every row unless the row's
+ * scores all sit at the bottom of the bound; such a row is written as zeros, never NaN); CP25_ERR_INVAL otherwise.
+ * o bf16. No reference counterpart; replaces the same attention call. */
 int cp25_attn_fwd_prescaled_fp8(const void* q8, const void* k8, const void* v8t, const float* v_amax, void* o, int B,
                                 int H, int Lq, int Lk, int D, const int64_t* q_strides, const int64_t* k_strides,
                                 const int64_t* o_strides, float q_norm_bound, float k_norm_bound, int n_split,
                                 void* workspace, size_t ws_bytes, hipStream_t stream);
+
+/* Name of the kernel form cp25_attn_fwd_bounded (prescaled = 0, fp8 = 0), _prescaled (prescaled = 1),
+ * _prescaled_fp8qk (fp8 = 1) or _prescaled_fp8 (fp8 = 2) launches for these arguments (a static string), e.g.
+ * "attn_fwd_m16<self, prescaled, online max>": what a bench or log reports as the kernel that ran. */
+const char* cp25_attn_kernel(int Lk, float softmax_scale, float q_norm_bound, float k_norm_bound, int prescaled,
+                             int fp8);
 
 /* Bytes of workspace cp25_attn_fwd_split / _bounded need (0 for n_split <= 1). */
 size_t cp25_attn_workspace_bytes(int B, int H, int Lq, int n_split);
@@ -196,8 +190,22 @@ int cp25_gelu(void* x, int64_t n, hipStream_t stream);
  * GPT2FeedForward layer1 + exact GELU (:227-254, CP25_EPI_GELU) and layer2. */
 #define CP25_EPI_NONE 0
 #define CP25_EPI_GELU 1
+#define CP25_EPI_RES 2
 int cp25_gemm_epi(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int M, int N, int K,
                   int epilogue, hipStream_t stream);
+
+/* cp25_gemm_epi with the block's gated residual as the epilogue: C = bf16(x + bf16(gate * bf16(A W^T))), the two
+ * bf16 roundings of the reference's `x + gate * y` (cp25_ln_mod's residual, bit for bit). Output row r is token
+ * tok = r / B, batch entry b = r % B of a token-major [n_tok, B, N] activation (B divides 16); x element
+ * (tok, b, col) at x + tok * x_st + b * x_sb + col (x_sb = 0 broadcasts one row over the batch), gate element
+ * (b, frame, col) at gate + b * g_sb + frame * g_st + col with frame = (tok0 + tok) / hw (tok0 = the CP shard's first
+ * token; hw >= 16 / B). All strides multiples of 8 elements, 16-B aligned bases. C may not alias x. The next cp25_ln_mod then
+ * runs with y = NULL on C.
+ * Replaces: the gated residuals of Block.forward (minimal_v4_dit.py:1204, :1237, :1246) fused into the output
+ * projection (:432), the cross-attention output projection and GPT2FeedForward layer2 (:227-254). */
+int cp25_gemm_res(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int M, int N, int K,
+                  const void* x, int64_t x_st, int64_t x_sb, const void* gate, int64_t g_sb, int64_t g_st, int B,
+                  int64_t tok0, int64_t hw, hipStream_t stream);
 
 /* Latents live in "patch layout" [n_tok, 64] fp32, element (tok, p*16 + c), p = p1*2 + p2 (the
  * final layer's "(p1 p2 t C)" order). cp25_patchify builds the x_embedder input rows [n_tok, 72]

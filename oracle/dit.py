@@ -19,6 +19,9 @@ TE RMSNorm (fp32 math, one rounding of (x*rstd)*w), TE fused RoPE (rotate-half, 
 (fp32 softmax, bf16 output).
 
 Config: a dict with the DiTConfig field names (cosmos_predict2/net_config.py).
+Device-agnostic torch code: the tests run it on the CPU, and at full-geometry sizes that would take hours on host
+cores (a 136 080-token multi-view block) on the GPU's own torch ops (fp32 matmuls), never on this repository's
+kernels.
 Weights: a state dict with the reference's `net.` key layout, bf16 tensors.
 """
 from __future__ import annotations
@@ -62,7 +65,7 @@ def te_rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-6) -> torch.Ten
     return ((xf * rstd) * w.float()).to(x.dtype)
 
 
-def rope_freqs(cfg: dict, T: int, H: int, W: int) -> torch.Tensor:
+def rope_freqs(cfg: dict, T: int, H: int, W: int, device="cpu") -> torch.Tensor:
     """VideoRopePosition3DEmb.generate_embeddings with bf16 buffers -> [T*H*W, 128] fp32."""
     dim = cfg["model_channels"] // cfg["num_heads"]
     dim_h = dim // 6 * 2
@@ -92,7 +95,7 @@ def rope_freqs(cfg: dict, T: int, H: int, W: int) -> torch.Tensor:
         * 2,
         dim=-1,
     )
-    return grid.reshape(T * H * W, dim).float()
+    return grid.reshape(T * H * W, dim).float().to(device)
 
 
 def apply_rope(x: torch.Tensor, freqs: torch.Tensor) -> torch.Tensor:
@@ -147,7 +150,7 @@ def timestep_embedding(cfg, sd, t_B_T: torch.Tensor, action: torch.Tensor | None
     the action embeddings before the norm (action_conditioned_minimal_v1_lvg_dit.py:298-305)."""
     D = cfg["model_channels"]
     half = D // 2
-    expo = -math.log(10000) * torch.arange(half, dtype=F32) / (half - 0.0)
+    expo = -math.log(10000) * torch.arange(half, dtype=F32, device=t_B_T.device) / (half - 0.0)
     emb = t_B_T.flatten().float()[:, None] * torch.exp(expo)[None, :]
     sincos = torch.cat([torch.cos(emb), torch.sin(emb)], dim=-1).reshape(t_B_T.shape[0], t_B_T.shape[1], D)
     h = F.silu(_lin(sincos, _w(sd, "t_embedder.1.linear_1.weight").float()))
@@ -234,13 +237,13 @@ def dit_forward(cfg: dict, sd: dict, x_B_C_T_H_W: torch.Tensor, timesteps_B_T: t
     x = torch.cat([x, cond_mask_B_1_T_H_W.to(act_dtype())], dim=1)  # minimal_v1_lvg_dit.py:46
     t = timesteps_B_T * cfg["timestep_scale"]
     if cfg["concat_padding_mask"]:
-        pm = padding_mask_B_1_H_W if padding_mask_B_1_H_W is not None else torch.zeros(B, 1, Hl, Wl)
+        pm = padding_mask_B_1_H_W if padding_mask_B_1_H_W is not None else torch.zeros(B, 1, Hl, Wl, device=x.device)
         pm = F.interpolate(pm.float(), size=(Hl, Wl), mode="nearest").to(act_dtype())
         x = torch.cat([x, pm[:, :, None].expand(B, 1, T, Hl, Wl)], dim=1)
     n_views = T // cfg["state_t"] if cfg.get("n_cameras_emb", 0) else 1
     if n_views > 1 or cfg.get("n_cameras_emb", 0):
         # concat_view_embedding (multiview_dit.py:462-490): view channels after [x, mask, padding mask]
-        vidx = torch.arange(n_views).clamp(max=cfg["n_cameras_emb"] - 1)
+        vidx = torch.arange(n_views, device=x.device).clamp(max=cfg["n_cameras_emb"] - 1)
         ve = _w(sd, "view_embeddings.weight")[vidx]  # [V, vdim] bf16
         Tv = T // n_views
         vch = ve.t()[None, :, :, None, None, None].expand(B, ve.shape[1], n_views, Tv, Hl, Wl)
@@ -252,7 +255,7 @@ def dit_forward(cfg: dict, sd: dict, x_B_C_T_H_W: torch.Tensor, timesteps_B_T: t
     xp = xp.reshape(B, Tp, Hp, Wp, -1)
     x = _lin(xp, _w(sd, "x_embedder.proj.1.weight"))
     # MultiCameraVideoRopePosition3DEmb (multiview_dit.py:108-130): positions restart per view
-    freqs = rope_freqs(cfg, Tp // n_views, Hp, Wp).repeat(n_views, 1)
+    freqs = rope_freqs(cfg, Tp // n_views, Hp, Wp, x.device).repeat(n_views, 1)
 
     ctx = crossattn_emb.to(act_dtype())
     if cfg["use_crossattn_projection"]:

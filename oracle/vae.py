@@ -9,14 +9,34 @@ Follows cosmos_predict2/_src/predict2/tokenizers/wan2pt1.py:
   Wan2pt1VAEInterface.encode/decode :998-1026 (img/video mean-std identity when load_mean_std=False).
 The model runs in bf16 (is_amp=False, wan2pt1.py:790-792): every op rounds to bf16 as torch does.
 Convolutions accumulate in fp32 (parity unpinned: cuDNN in the reference).
+fp32_truth(): the same restatement over the same bf16 weights with every activation kept in fp32 (no intermediate
+bf16 rounding): the exact-math scale both the bf16 reference and the HIP path are measured against.
+Device-agnostic torch code: the tests run it on the CPU, and at the 704 x 1280 geometry (minutes on host cores) on the
+GPU's own torch ops (MIOpen / hipBLASLt in fp32), never on this repository's kernels.
 """
 from __future__ import annotations
+
+import contextlib
 
 import torch
 import torch.nn.functional as F
 
 BF16 = torch.bfloat16
 CACHE_T = 2
+_ACT = [BF16]  # activation dtype: bf16 = the reference's arithmetic; fp32 inside fp32_truth()
+
+
+def act_dtype() -> torch.dtype:
+    return _ACT[-1]
+
+
+@contextlib.contextmanager
+def fp32_truth():
+    _ACT.append(torch.float32)
+    try:
+        yield
+    finally:
+        _ACT.pop()
 
 MEAN = [-0.7571, -0.7089, -0.9113, 0.1075, -0.1745, 0.9653, -0.1517, 1.5508,
         0.4134, -0.0715, 0.5517, -0.3632, -0.1922, -0.9497, 0.2503, -0.2921]
@@ -98,7 +118,7 @@ def attn_block(sd, p, x):
     qkv = qkv.reshape(b * t, 1, c * 3, -1).permute(0, 1, 3, 2).contiguous()
     q, k, v = qkv.chunk(3, dim=-1)
     s = torch.matmul(q.float(), k.float().transpose(-1, -2)) * (c ** -0.5)
-    o = torch.matmul(torch.softmax(s, -1), v.float()).to(BF16)
+    o = torch.matmul(torch.softmax(s, -1), v.float()).to(x.dtype)
     o = o.squeeze(1).permute(0, 2, 1).reshape(b * t, c, h, w)
     o = _conv2d(o, sd[p + ".proj.weight"], sd[p + ".proj.bias"])
     o = o.reshape(b, t, c, h, w).permute(0, 2, 1, 3, 4)
@@ -203,15 +223,16 @@ def decoder3d(sd, x, cache):
     return _cached_conv(sd, "decoder.head.2", x, cache)
 
 
-def _scale():
-    mean = torch.tensor(MEAN, dtype=BF16)
-    std = torch.tensor(STD, dtype=BF16)
+def _scale(device="cpu"):
+    # the buffers are bf16 in the reference (the whole VAE is cast to bf16); the truth keeps those values
+    mean = torch.tensor(MEAN, dtype=BF16).to(device=device, dtype=act_dtype())
+    std = torch.tensor(STD, dtype=BF16).to(device=device, dtype=act_dtype())
     return mean, 1.0 / std
 
 
 def encode(sd, video: torch.Tensor, temporal_window: int = 16) -> torch.Tensor:
     """video [B, 3, T, H, W] in [-1, 1] -> latent mu [B, 16, 1 + (T-1)//4, H/8, W/8] (bf16)."""
-    x = video.to(BF16)
+    x = video.to(BF16).to(act_dtype())  # the same (bf16-valued) input pixels in both modes
     t = x.shape[2]
     cache = _Cache()
     outs = []
@@ -228,14 +249,14 @@ def encode(sd, video: torch.Tensor, temporal_window: int = 16) -> torch.Tensor:
         outs.append(encoder3d(sd, x[:, :, 1 + temporal_window * (n_iter - 1):], cache))
     out = torch.cat(outs, 2)
     mu = _conv3d(out, sd["conv1.weight"], sd["conv1.bias"], 0).chunk(2, dim=1)[0]
-    mean, inv_std = _scale()
+    mean, inv_std = _scale(mu.device)
     return (mu - mean.view(1, 16, 1, 1, 1)) * inv_std.view(1, 16, 1, 1, 1)
 
 
 def decode(sd, z: torch.Tensor) -> torch.Tensor:
     """latent [B, 16, T, h, w] -> video [B, 3, 1 + 4 (T-1), 8h, 8w] (bf16, ~[-1, 1])."""
-    mean, inv_std = _scale()
-    z = z.to(BF16)
+    mean, inv_std = _scale(z.device)
+    z = z.to(act_dtype())
     z = z / inv_std.view(1, 16, 1, 1, 1) + mean.view(1, 16, 1, 1, 1)
     x = _conv3d(z, sd["conv2.weight"], sd["conv2.bias"], 0)
     cache = _Cache()

@@ -90,16 +90,10 @@ def test_cast_v_fp8t_layout_bit_exact(device):
 
 @pytest.mark.parametrize("B,H,L,Lk,split", [(1, 2, 1000, 1000, None), (2, 4, 4800, 4800, None),
                                              (1, 3, 333, 1111, 3), (1, 2, 64, 4097, 5)])
-@pytest.mark.parametrize("pmode", ["int", "exact"])
-def test_attn_fp8_full_vs_fp32(device, monkeypatch, B, H, L, Lk, split, pmode):
+def test_attn_fp8_full_vs_fp32(device, B, H, L, Lk, split):
     """cp25_attn_fwd_prescaled_fp8 (e4m3 Q K^T, e5m2 P, e4m3 V): exact against fp32 math on the same quantised
-    operands, and the format's cost against fp32 on the bf16 inputs. pmode "int" (the default kernel): the e5m2
-    byte of P is round(4 (S - shift) + 60) read as e5m2, the row sums those P's; "exact" (CP25_F8_EXP=exact):
-    P = exp2(S - shift) rounded to e5m2, the row sums of the unrounded P. V goes through v8t's per-head scale."""
-    if pmode == "exact":
-        monkeypatch.setenv("CP25_F8_EXP", "exact")
-    else:
-        monkeypatch.delenv("CP25_F8_EXP", raising=False)
+    operands, and the format's cost against fp32 on the bf16 inputs. The e5m2 byte of P is round(4 (S - shift) + 60)
+    read as e5m2, the row sums those P's. V goes through v8t's per-head scale."""
     q = _normed((B, L, H, 128), 1, device)
     k = _normed((B, Lk, H, 128), 2, device)
     v = torch.randn((B, Lk, H, 128), device=device, generator=torch.Generator(device=device).manual_seed(3)).to(torch.bfloat16)
@@ -113,22 +107,40 @@ def test_attn_fp8_full_vs_fp32(device, monkeypatch, B, H, L, Lk, split, pmode):
     qd = q8.view(torch.float8_e4m3fn).float() / QS
     kd = k8.view(torch.float8_e4m3fn).float() * QS
     s = torch.einsum("bqhd,bkhd->bhqk", qd, kd) - shift  # log2 units
-    if pmode == "exact":
-        p = torch.exp2(s)
-        p8 = p.to(torch.float8_e5m2).float()
-    else:
-        p8 = torch.round(4 * s + 60).clamp(0, 255).to(torch.uint8).view(torch.float8_e5m2).float()
-        p = p8
+    p8 = torch.round(4 * s + 60).clamp(0, 255).to(torch.uint8).view(torch.float8_e5m2).float()
     sc = (amax / 448.0).view(B, H)
     vd = ((v.float() / sc.view(B, 1, H, 1)).clamp(-448, 448).to(torch.float8_e4m3fn).float()) * sc.view(B, 1, H, 1)
-    emu = torch.einsum("bhqk,bkhd->bqhd", p8, vd) / p.sum(-1).permute(0, 2, 1)[..., None]
+    emu = torch.einsum("bhqk,bkhd->bqhd", p8, vd) / p8.sum(-1).permute(0, 2, 1)[..., None]
     s32 = torch.einsum("bqhd,bkhd->bhqk", q.float(), k.float()) * 128 ** -0.5
     full = torch.einsum("bhqk,bkhd->bqhd", torch.softmax(s32, -1), v.float())
     rel = lambda o, r: ((o.float() - r).norm() / r.norm()).item()  # noqa: E731
     e_emu, e_full = rel(o8, emu), rel(o8, full)
-    print(f"fp8 attention ({pmode} P) B={B} H={H} Lq={L} Lk={Lk} split={split}: vs fp32 on the quantised operands {e_emu:.2e}, "
+    print(f"fp8 attention B={B} H={H} Lq={L} Lk={Lk} split={split}: vs fp32 on the quantised operands {e_emu:.2e}, "
           f"vs fp32 {e_full:.2e}")
     assert torch.isfinite(o8.float()).all()
     assert e_emu <= 4e-3, e_emu
     # e5m2 P (2 mantissa bits) + e4m3 Q K^T + e4m3 V on random, near-uniform attention
     assert e_full <= 1e-1, e_full
+
+
+@pytest.mark.parametrize("split", [None, 4])
+def test_attn_fp8_window_edges(device, split):
+    """The fp8 P.V window: at the largest allowed bound product (1.13 x it = 30, shift 15) rows whose every
+    score sits at the bottom of the window underflow to P = 0 and must come out as zeros (an empty split partial),
+    never NaN; beyond the window the library refuses the form (the DiT then runs fp8 Q K^T with bf16 P.V)."""
+    B, H, L = 1, 1, 256
+    qb = kb = (29.9 / 1.13) ** 0.5
+    g = torch.Generator().manual_seed(9)
+    u = torch.randn(128, generator=g)
+    u = u / u.norm()
+    qs = (torch.randn(B, L, H, 128, generator=g) * 0.01 + u * qb * 0.99).to(device, torch.bfloat16)
+    k = (-u * kb * 0.99).expand(B, L, H, 128).contiguous().to(device, torch.bfloat16)  # every score ~ -26
+    v = torch.randn(B, L, H, 128, generator=g).to(device, torch.bfloat16)
+    q8 = N.cast_fp8(qs.reshape(-1, 128), QS).view(B, L, H, 128)
+    k8 = N.cast_fp8(k.reshape(-1, 128), 1.0 / QS).view(B, L, H, 128)
+    v8t, amax = N.cast_v_fp8t(v)
+    o8 = N.attn_fwd(qs, k, v, norm_bounds=(qb, kb), prescaled=True, fp8_qk=(q8, k8), fp8_v=(v8t, amax), n_split=split)
+    torch.cuda.synchronize()
+    assert torch.isfinite(o8.float()).all()
+    with pytest.raises(ValueError):
+        N.attn_fwd(qs, k, v, norm_bounds=(qb * 1.1, kb), prescaled=True, fp8_qk=(q8, k8), fp8_v=(v8t, amax))

@@ -17,6 +17,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import __graft_entry__  # noqa: F401
+from cosmos_predict2 import _native as N  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -139,7 +140,7 @@ def _worker(rank, world, port, q_out):
 def test_attn_op_context_parallel_matches_single_rank(device, monkeypatch):
     from cosmos_predict2.attn_op import CP25AttnOp
 
-    monkeypatch.setenv("CP25_ATTN_SPLIT", "1")
+    monkeypatch.setattr(N, "_ATTN_SPLIT", 1)
     q, k, v = _case()
     ref = CP25AttnOp()(q.to(device), k.to(device), v.to(device)).cpu().float()
     ctx = mp.get_context("spawn")

@@ -116,16 +116,52 @@ def test_full_depth_2b_forward_fp8_modes(device, net2b):
         assert dist[key]["hip_truth"] <= 7e-2, dist
 
 
+def test_full_depth_2b_forward_trained_size_norm_weights(device, net2b):
+    """The 28-block forward with every q/k RMSNorm weight uniform in [0.5, 3] (trained-checkpoint scale, SURVEY A14;
+    minimal_v4_dit.py:355-358): the weight bound product is ~150 log2 units, past the fixed-shift range, so every
+    self- and cross-attention runs the online-max form (the report names it). Same truth gate as the unit weights."""
+    cfg, sd0 = net2b
+    g = torch.Generator().manual_seed(41)
+    sd = dict(sd0)
+    for k in sd:
+        if k.endswith(("q_norm.weight", "k_norm.weight")):
+            sd[k] = (0.5 + 2.5 * torch.rand(sd[k].shape, generator=g)).to(torch.bfloat16)
+    T, H, W = 3, 32, 32
+    x = torch.randn(1, 16, T, H, W, generator=g)
+    mask = torch.zeros(1, 1, T, H, W)
+    mask[:, :, :1] = 1
+    t = torch.tensor([[0.1, 877.0, 877.0]])
+    ctx = torch.randn(1, 512, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
+    c = dataclasses.asdict(cfg)
+    ref = odit.dit_forward(c, sd, x, t, ctx, mask)
+    with odit.fp32_truth():
+        truth = odit.dit_forward(c, sd, x, t, ctx, mask)
+    net = MinimalV1LVGDiT(cfg, device=device)
+    net.load_state_dict(sd)
+    kern = net.attention_kernels(T * H * W // 4)
+    print("attention kernels:", kern)
+    assert "online" in kern["self"] and "online" in kern["cross"], kern
+    hip = net(x.to(device).to(torch.bfloat16), t.to(device), ctx.to(device),
+              condition_video_input_mask_B_C_T_H_W=mask.to(device)).cpu()
+    d = _report("28-block 2B forward, q/k norm weights in [0.5, 3]", hip, ref, truth)
+    assert torch.isfinite(hip).all()
+    assert d["hip_truth"] <= 1.1 * d["ref_truth"], d
+    assert d["hip_ref"] <= 2e-2, d
+
+
 @pytest.mark.parametrize("guidance", [0.0, 7.0])
 def test_full_depth_2b_sampler(device, net2b, guidance):
-    """Karras 2 steps (3 evaluations x CFG) of the 28-block 2B net at config-1 geometry, the metric's
-    guidance 7 and guidance 0."""
+    """Karras 2 steps (3 evaluations x CFG) of the 28-block 2B net at config-1 geometry, the metric's guidance 7 and
+    guidance 0. The uncond branch gets the reference's context for is_negative_prompt=False: a zeroed embedding
+    (TextAttr dropout, video2world_model_rectified_flow.py:167-170; model.py begin_sampling_from_batch), so c and u
+    differ as they do in the metric run and c + 7 (c - u) does not amplify rounding noise ~15x the way two random
+    contexts (c ~ u) would."""
     cfg, sd = net2b
     T, H, W = 3, 32, 32
     g = torch.Generator().manual_seed(71)
     gt = torch.randn(1, 16, T, H, W, generator=g)
     ctx_c = torch.randn(1, 512, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
-    ctx_u = torch.randn(1, 512, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
+    ctx_u = torch.zeros_like(ctx_c)
     c = dataclasses.asdict(cfg)
     kw = dict(num_cond=1, guidance=guidance, seed=0, num_steps=2, use_karras=True, cond_frame_t=0.1)
     ref = osamp.generate(c, sd, gt, ctx_c, ctx_u, **kw)
@@ -138,8 +174,7 @@ def test_full_depth_2b_sampler(device, net2b, guidance):
                                num_conditional_frames=1, guidance=guidance, seed=0, num_steps=2).cpu()
     d = _report(f"28-block 2B sampler, Karras 2 steps, g={guidance}", hip, ref, truth)
     assert torch.isfinite(hip).all()
-    # measured (MI355X, round 2): g=0 hip-truth 1.567e-2, ref-truth 1.563e-2, hip-ref 1.274e-2;
-    # g=7 1.421e-1, 1.425e-1, 1.376e-1 (c + 7 (c - u) amplifies the per-branch bf16 error ~15x:
-    # random text contexts make c and u differ by only ~2.5 %, tools/diag_batch.py)
+    # measured (MI355X, round 2, random uncond context): g=0 hip-truth 1.567e-2, ref-truth 1.563e-2, hip-ref
+    # 1.274e-2; g=7 1.421e-1, 1.425e-1, 1.376e-1 (c ~ u: 7 (c - u) amplified the per-branch bf16 error ~15x)
     assert d["hip_truth"] <= 1.1 * d["ref_truth"], d
-    assert d["hip_ref"] <= (1.6e-2 if guidance == 0 else 1.8e-1), d
+    assert d["hip_ref"] <= (1.6e-2 if guidance == 0 else 6e-2), d

@@ -92,32 +92,76 @@ def vae_pair():
     return sd
 
 
+def _report(name, hip, ref, truth):
+    d = dict(hip_truth=rel_l2(hip, truth), ref_truth=rel_l2(ref, truth), hip_ref=rel_l2(hip, ref))
+    print(f"{name}: hip-vs-truth {d['hip_truth']:.3e}  bf16ref-vs-truth {d['ref_truth']:.3e}  "
+          f"hip-vs-bf16ref {d['hip_ref']:.3e}")
+    return d
+
+
 def test_vae_encode_matches_oracle(device, vae_pair):
+    """Encode (9 frames, 64 x 96) against the bf16 oracle and the fp32 truth (oracle.vae.fp32_truth: the same bf16
+    weights, every activation fp32). The gate is the DiT's: the HIP path no further from the truth than the bf16
+    reference restatement is (x 1.1); hip-vs-ref bounded by the measured value."""
     sd = vae_pair
     g = torch.Generator().manual_seed(7)
     video = (torch.rand(1, 3, 9, 64, 96, generator=g) * 2 - 1).to(torch.bfloat16)
     ref = ovae.encode(sd, video, temporal_window=4)
+    with ovae.fp32_truth():
+        truth = ovae.encode(sd, video, temporal_window=4)
     tok = Wan2pt1VAEInterface(sd, device=device, temporal_window=4)
     out = tok.encode(video.to(device))
     torch.cuda.synchronize()
     assert out.shape == ref.shape, (out.shape, ref.shape)
-    err = rel_l2(out.cpu(), ref)
-    print(f"vae encode rel-L2: {err:.3e}")
-    assert err <= 2e-2, err
+    d = _report("vae encode 9f 64x96", out.cpu(), ref, truth)
+    # measured (MI355X, round 2): hip-vs-ref 7.6e-3
+    assert d["hip_truth"] <= 1.1 * d["ref_truth"], d
+    assert d["hip_ref"] <= 2e-2, d
 
 
 def test_vae_decode_matches_oracle(device, vae_pair):
+    """Decode of a 3 x 8 x 12 latent against the bf16 oracle and the fp32 truth (gate as for encode)."""
     sd = vae_pair
     g = torch.Generator().manual_seed(8)
     z = torch.randn(1, 16, 3, 8, 12, generator=g)
     ref = ovae.decode(sd, z)
+    with ovae.fp32_truth():
+        truth = ovae.decode(sd, z)
     tok = Wan2pt1VAEInterface(sd, device=device)
     out = tok.decode(z.to(device))
     torch.cuda.synchronize()
     assert out.shape == ref.shape, (out.shape, ref.shape)
-    err = rel_l2(out.cpu(), ref)
-    print(f"vae decode rel-L2: {err:.3e}")
-    assert err <= 2e-2, err
+    d = _report("vae decode 3x8x12", out.cpu(), ref, truth)
+    # measured (MI355X, round 2): hip-vs-ref 1.3e-2
+    assert d["hip_truth"] <= 1.1 * d["ref_truth"], d
+    assert d["hip_ref"] <= 2e-2, d
+
+
+def test_vae_decode_metric_geometry(device):
+    """BASELINE config 2's decode geometry: 2 latent frames at 88 x 160 -> 5 frames at 704 x 1280
+    (wan2pt1.py:551-570, WanVAE_.decode one latent frame at a time with the causal cache). The oracle at this size is
+    ~4.5e13 FLOP (minutes on host cores), so the restatement runs on the GPU's own torch ops (fp32 MIOpen convs,
+    fp32 matmuls), in bf16-reference mode and in fp32-truth mode; the HIP path (cp25_conv3d halo / per-tap convs,
+    cp25_vae_attn, cp25_rms_norm_silu) must be as close to the truth as the bf16 reference is."""
+    sd = init_vae_state_dict(seed=3)
+    sdd = {k: v.to(device) for k, v in sd.items()}
+    g = torch.Generator().manual_seed(12)
+    z = torch.randn(1, 16, 2, 88, 160, generator=g).to(device)
+    tok = Wan2pt1VAEInterface(sd, device=device)
+    out = tok.decode(z)
+    torch.cuda.synchronize()
+    assert out.shape == (1, 3, 5, 704, 1280), out.shape
+    with torch.no_grad():
+        ref = ovae.decode(sdd, z)
+        with ovae.fp32_truth():
+            truth = ovae.decode(sdd, z)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out.float()).all()
+    d = _report("vae decode 2x88x160 -> 5f 704x1280", out.float(), ref.float(), truth.float())
+    per_frame = [rel_l2(out[:, :, f].float(), ref[:, :, f].float()) for f in range(5)]
+    print("  per output frame hip-vs-bf16ref: " + " ".join(f"{e:.2e}" for e in per_frame))
+    assert d["hip_truth"] <= 1.1 * d["ref_truth"], d
+    assert d["hip_ref"] <= 3e-2, d
 
 
 def test_first_frame_encode_is_causal_prefix(device, vae_pair):

@@ -31,6 +31,8 @@ def main():
                     help="RMS-normalised q/k rows (as the DiT's q/k norm leaves them) and their norm bounds: the "
                          "bounded-shift softmax (cp25_attn_fwd_bounded)")
     ap.add_argument("--normed", action="store_true", help="RMS-normalised q/k rows without passing the bounds")
+    ap.add_argument("--wrange", default="1,1", help="lo,hi: q/k RMSNorm weights uniform in [lo, hi] (seeded; 1,1 = the "
+                    "unit init weights); --bounded passes the DiT's weight bounds sqrt(128) max|w| 1.02")
     ap.add_argument("--prescaled", action="store_true",
                     help="with --bounded: q carries scale*log2(e) (the DiT's default form, cp25_attn_fwd_prescaled)")
     ap.add_argument("--fp8qk", action="store_true",
@@ -58,14 +60,17 @@ def main():
             t.zero_()
     nb = None
     if a.bounded or a.normed:
-        for t in (q, k):  # RMSNorm with unit weight, in place, per head row
-            t.copy_((t.float() * torch.rsqrt(t.float().pow(2).mean(-1, keepdim=True) + 1e-6)).to(torch.bfloat16))
-        nb = (128 ** 0.5 * 1.02, 128 ** 0.5 * 1.02) if a.bounded else None
+        lo, hi = (float(x) for x in a.wrange.split(","))
+        w = lo + (hi - lo) * torch.rand(128, device=dev, generator=torch.Generator(device=dev).manual_seed(5))
+        for t in (q, k):  # RMSNorm with weight w, in place, per head row
+            t.copy_((t.float() * torch.rsqrt(t.float().pow(2).mean(-1, keepdim=True) + 1e-6) * w).to(torch.bfloat16))
+        wb = 128 ** 0.5 * float(w.abs().max()) * 1.02
+        nb = (wb, wb) if a.bounded else None
     pre = {}
     if a.prescaled:
         c = 128 ** -0.5 * 1.4426950408889634
         q.copy_((q.float() * c).to(torch.bfloat16))
-        nb = (nb[0] * c, nb[1])
+        nb = (nb[0] * c, nb[1]) if nb else None
         pre = dict(prescaled=True)
         if a.fp8qk:
             if a.fused:
@@ -100,7 +105,7 @@ def main():
     ms = e0.elapsed_time(e1) / a.iters
     flop = 4.0 * a.B * a.H * a.L * Lk * 128
     print(json.dumps({"kernel": "attn_fwd", "B": a.B, "H": a.H, "Lq": a.L, "Lk": Lk, "fused": a.fused,
-                      "zeros": a.zeros, "bounded": a.bounded, "prescaled": a.prescaled, "fp8qk": a.fp8qk, "fp8pv": a.fp8pv, "normed": a.normed or a.bounded, "split": ns, "iters": a.iters, "lib": os.path.basename(a.lib) or "libcp25.so", "ms": ms,
+                      "zeros": a.zeros, "bounded": a.bounded, "prescaled": a.prescaled, "fp8qk": a.fp8qk, "fp8pv": a.fp8pv, "normed": a.normed or a.bounded, "wrange": a.wrange, "split": ns, "iters": a.iters, "lib": os.path.basename(a.lib) or "libcp25.so", "ms": ms,
                       "tflops": flop / ms / 1e9, "check_rel_l2": check}))
 
 
