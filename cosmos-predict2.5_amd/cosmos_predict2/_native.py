@@ -13,7 +13,8 @@ from typing import Optional, Tuple
 
 import torch
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libcp25.so")
+_DEFAULT_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libcp25.so")
+_LIB_PATH = _DEFAULT_LIB_PATH
 _lib: Optional[ctypes.CDLL] = None
 
 c_int64_p = ctypes.POINTER(ctypes.c_int64)
@@ -74,6 +75,9 @@ SIGNATURES = {
     "cp25_gelu": [_P, _I64, _P],
     "cp25_gemm_epi": [_P, _I64, _P, _I64, _P, _I64, _I, _I, _I, _I, _P],
     "cp25_gemm_res": [_P, _I64, _P, _I64, _P, _I64, _I, _I, _I, _P, _I64, _I64, _P, _I64, _I64, _I, _I64, _I64, _P],
+    "cp25_gemm_fp8": [_P, _I64, _P, _P, _I64, _P, _P, _I64, _I, _I, _I, _P],
+    "cp25_gemm_fp8_res": [_P, _I64, _P, _P, _I64, _P, _P, _I64, _I, _I, _I, _P, _I64, _I64, _P, _I64, _I64, _I, _I64,
+                          _I64, _P],
     "cp25_quant_fp8_rows": [_P, _P, _P, _I64, _I64, _P],
     "cp25_gelu_quant_fp8": [_P, _P, _P, _I64, _I64, _P],
     "cp25_patchify": [_P, _P, _P, _P, _P, _I64, _I64, _I64, _P],
@@ -82,6 +86,7 @@ SIGNATURES = {
     "cp25_conv3d": [ctypes.POINTER(ctypes.c_void_p), _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I,
                     _I, _I, _I, _I, _I, _I, _P],
     "cp25_rms_norm_silu": [_P, _P, _P, _I64, _I, _I, _P],
+    "cp25_conv3d_select": [_I],
     "cp25_softmax_rows": [_P, _I64, _I, _I64, _F, _P, _I64, _P],
     "cp25_vae_attn": [_P, _I64, _I64, _P, _I64, _I64, _P, _I64, _I64, _P, _I64, _I64, _I, _I, _I, _I, _F, _P, _I64,
                       _P],
@@ -104,10 +109,11 @@ def load_library() -> ctypes.CDLL:
             "(or __graft_entry__.build()). There is no non-native fallback."
         )
     lib = ctypes.CDLL(_LIB_PATH)
+    lab = os.path.abspath(_LIB_PATH) != os.path.abspath(_DEFAULT_LIB_PATH)  # an A/B build (tools/lab): may predate symbols
     for name, argtypes in SIGNATURES.items():
         fn = getattr(lib, name, None)
         if fn is None:
-            if argtypes is None:
+            if argtypes is None or lab:
                 continue
             raise RuntimeError(f"libcp25.so does not export {name}")
         if argtypes is not None:
@@ -176,7 +182,7 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
     """softmax(q k^T * scale) v for q [B, Lq, H, 128], k/v [B, Lk, H, 128] (bf16, any strides with
     a contiguous head dim). Returns [B, Lq, H, 128] bf16. n_split: key-range split (None = the
     library's plan for this shape; the fp32 partials live in a caching-allocator workspace).
-    norm_bounds: (max |q|, max |k|) upper bounds over all rows: where max|q| max|k| (in log2 units) <= 80 the
+    norm_bounds: (max |q|, max |k|) upper bounds over all rows: where max|q| max|k| (in log2 units) <= 98 the
     rows use a fixed softmax shift, else (or None) an online row max (cp25_attn_fwd_bounded; any data).
     prescaled=True: q rows already carry scale * log2(e) (head_rmsnorm_rope(out_scale=...)); norm_bounds (of the
     scaled q and of k) optional as above (cp25_attn_fwd_prescaled; softmax_scale unused).
@@ -447,6 +453,46 @@ def gemm_res(a: torch.Tensor, w: torch.Tensor, x: torch.Tensor, x_st: int, x_sb:
     return out
 
 
+def gemm_fp8_supported(N: int, K: int) -> bool:
+    """Shapes cp25_gemm_fp8 is built for (N multiple of 256, K of 256); others stay on torch._scaled_mm."""
+    return N % 256 == 0 and K % 256 == 0
+
+
+def gemm_fp8(q: torch.Tensor, s: torch.Tensor, w8: torch.Tensor, ws: torch.Tensor, *, res=None,
+             out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bf16 (q[M, K] w8[N, K]^T) * s[m] * ws[n] on the hand-written fp8 GEMM (cp25_gemm_fp8: torch._scaled_mm's
+    row / column-scaled definition). q, w8 float8_e4m3fn (K contiguous), s [M, 1] / ws [1, N] (or [N]) fp32.
+    res = (x, x_st, x_sb, gate, B, tok0, hw): the gated-residual epilogue of gemm_res (cp25_gemm_fp8_res)."""
+    lib = load_library()
+    if q.dtype != torch.float8_e4m3fn or w8.dtype != torch.float8_e4m3fn:
+        raise ValueError("gemm_fp8 expects float8_e4m3fn operands")
+    if q.dim() != 2 or w8.dim() != 2 or q.shape[1] != w8.shape[1] or q.stride(1) != 1 or w8.stride(1) != 1:
+        raise ValueError(f"gemm_fp8 shapes q{tuple(q.shape)} w{tuple(w8.shape)}")
+    M, K = q.shape
+    Nn = w8.shape[0]
+    if s.dtype != torch.float32 or ws.dtype != torch.float32 or s.numel() != M or ws.numel() != Nn or \
+            not s.is_contiguous() or not ws.is_contiguous():
+        raise ValueError("gemm_fp8 scales: contiguous fp32 [M] rows and [N] columns")
+    if out is None:
+        out = torch.empty((M, Nn), dtype=torch.bfloat16, device=q.device)
+    if tuple(out.shape) != (M, Nn) or out.stride(1) != 1 or out.dtype != torch.bfloat16:
+        raise ValueError(f"gemm_fp8 out {tuple(out.shape)} != ({M}, {Nn})")
+    if res is None:
+        rc = lib.cp25_gemm_fp8(_ptr(q), q.stride(0), _ptr(s), _ptr(w8), w8.stride(0), _ptr(ws), _ptr(out), out.stride(0),
+                               M, Nn, K, _stream(q.device))
+        _check("cp25_gemm_fp8", rc)
+        return out
+    x, x_st, x_sb, gate, B, tok0, hw = res
+    if x.dtype != torch.bfloat16 or gate.dtype != torch.bfloat16 or gate.dim() != 3 or gate.stride(2) != 1:
+        raise ValueError("gemm_fp8 res: bf16 x and a [B, T, N] bf16 gate view")
+    _check_frames(gate, n_tok=M // B, B=B, tok0=tok0, hw=hw)
+    rc = lib.cp25_gemm_fp8_res(_ptr(q), q.stride(0), _ptr(s), _ptr(w8), w8.stride(0), _ptr(ws), _ptr(out),
+                               out.stride(0), M, Nn, K, _ptr(x), x_st, x_sb, _ptr(gate), gate.stride(0), gate.stride(1),
+                               B, tok0, hw, _stream(q.device))
+    _check("cp25_gemm_fp8_res", rc)
+    return out
+
+
 def quant_fp8_rows(x: torch.Tensor, gelu: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
     """Row-scaled fp8 (float8_e4m3fn) operand of x [M, K] bf16: returns (q [M, K], scale [M, 1] fp32) with
     x ~= q * scale (of GELU(x) when gelu=True). cp25_quant_fp8_rows / cp25_gelu_quant_fp8."""
@@ -513,6 +559,14 @@ def conv3d(frames, weight: torch.Tensor, bias: Optional[torch.Tensor], out: torc
                          out_split, _stream(dev))
     _check("cp25_conv3d", rc)
     return out
+
+
+def conv3d_select(mode: int) -> int:
+    """cp25_conv3d_select: 0 = the halo kernel for 3x3 stride-1 convs (default), 1 = the per-tap kernel everywhere
+    (A/B and tests). Returns the previous mode."""
+    rc = load_library().cp25_conv3d_select(int(mode))
+    _check("cp25_conv3d_select", min(rc, 0))
+    return rc
 
 
 def rms_norm_silu(x: torch.Tensor, gamma: torch.Tensor, silu: bool = True, out: Optional[torch.Tensor] = None):

@@ -65,8 +65,9 @@ class _GlooDeferred:
     gathered bytes in `out` on the CURRENT stream, so `out` is written only after wait() -- the ordering RCCL's
     async work gives the lanes of run_lanes (the other lane's block is queued between issue and wait)."""
 
-    def __init__(self, out: torch.Tensor, parts, work, w: int, row_shape):
-        self.out, self.parts, self.work, self.w, self.row_shape = out, parts, work, w, row_shape
+    def __init__(self, out: torch.Tensor, src: torch.Tensor, parts, work, w: int, row_shape):
+        # src (the staged shard) and parts stay referenced until wait(): the async gloo work reads / writes them
+        self.out, self.src, self.parts, self.work, self.w, self.row_shape = out, src, parts, work, w, row_shape
 
     def wait(self) -> bool:
         self.work.wait()
@@ -84,7 +85,7 @@ def all_gather_into_async(out: torch.Tensor, x: torch.Tensor, group):
         xc = x.detach().contiguous().cpu()
         parts = [torch.empty_like(xc) for _ in range(w)]
         work = dist.all_gather(parts, xc, group=group, async_op=True)
-        return _GlooDeferred(out, parts, work, w, tuple(xc.shape[1:]))
+        return _GlooDeferred(out, xc, parts, work, w, tuple(xc.shape[1:]))
     w = dist.get_world_size(group)
     return dist.all_gather_into_tensor(out.view((w * x.shape[0],) + tuple(x.shape[1:])), x.contiguous(),
                                        group=group, async_op=True)

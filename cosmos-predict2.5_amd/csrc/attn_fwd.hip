@@ -10,7 +10,7 @@
 //                 K/V 64-key tiles double-buffered in padded LDS rows, counted-lgkmcnt operand ring, row sums by
 //                 MFMA, XCD-aware grid. The softmax shift of a query row enters as the initial C of its Q K^T MFMA
 //                 chains, so P = exp2(S) needs no per-score VALU beyond the exp (prescaled q). The shift is either
-//                 fixed from a norm bound (b_row = |q_row| max|k| <= 80: shift max(b_row - 60, 0), no max at all) or
+//                 fixed from a norm bound (b_row = |q_row| max|k| <= 98: shift max(b_row - 96, 0), no max at all) or
 //                 an online row max with lazy rescale (any data; per wave, decided at the kernel start).
 //   attn_fwd_f8   the config-5 fp8 option (no reference counterpart): Q K^T on v_mfma_f32_32x32x64_f8f6f4 over e4m3
 //                 q / k, and with kF8 = 3 also P.V on e5m2 P (made without exp2) and e4m3 V^T tiles.
@@ -32,9 +32,12 @@ constexpr int kQRows = 32;     // query rows per wave
 constexpr int kQBlk = kWaves * kQRows;  // 256 query rows per workgroup
 constexpr int kKBlk = 64;      // keys per tile
 constexpr int kThreads = kWaves * 64;
-constexpr float kTop = 60.f;        // fixed shift: largest exponent a term may reach (log2 units)
-constexpr float kMaxBound = 80.f;   // fixed shift: largest score bound b (smallest row-max term 2^(60 - 2 b) >= 2^-100)
-constexpr float kLazy = 8.f;        // online max: rescale only when a row max exceeds the shift by more (P <= 2^8)
+// Softmax-shift ranges (log2 units). A term is 2^(s - shift); the row sum of up to ~1.4e5 keys of 2^96 stays far inside
+// fp32 (1e34 < 3.4e38, and O = sum P v below it for |v| up to 3e4), bf16 P has the fp32 exponent range.
+constexpr float kTop = 96.f;        // zero / fixed shift: largest exponent a term may reach
+constexpr float kMaxBound = 98.f;   // fixed shift: largest score bound b (smallest row-max term 2^(96 - 2 b) >= 2^-100)
+constexpr float kTopF8 = 60.f;      // fp8 Q K^T form: P = exp2(S) unshifted for bound products up to this
+constexpr float kLazy = 24.f;       // online max: rescale only when a row max exceeds the shift by more (P <= 2^24)
 
 typedef __attribute__((address_space(3))) const char* lds_char_ptr;
 
@@ -107,13 +110,14 @@ struct AttnArgs {
 // Softmax shift (per query row, log2 units). Softmax is shift invariant; the shift only has to keep every term in
 // the fp32 / bf16 range. With a pre-scaled q (rows carry softmax_scale * log2 e) the shift is the initial C of the
 // row's Q K^T chains, so S arrives already shifted:
-//   fixed  (kbound given and b_row = |q_row| kbound <= 80 for every row of the wave): shift max(b_row - 60, 0);
-//          terms in [2^(60 - 2 b_row), 2^60], the row's largest >= 2^-100; no max reduction, no rescale;
-//   online (otherwise): tile 0 sets the shift to the row max; a later tile rescales O and the row sum (and moves the
-//          shift) only for a row whose max exceeds the shift by more than kLazy (8), so P <= 2^8 and the row's largest
-//          term >= 1. Per tile: 16 v_max3 + two row swaps per lane pair, the rescale itself is rare (a wave-uniform
-//          branch; rows below the threshold take it with d = 0, exactly, so rows stay independent of each other).
-// The mode is wave-uniform and chosen once at the kernel start from the wave's own |q_row|.
+//   zero   (pre-scaled q, bound product b <= 96): no shift; terms in [2^-b, 2^b];
+//   fixed  (b <= 98): shift max(b_row - 96, 0) from the row's own |q_row|; the row's largest term >= 2^-100;
+//   online (larger or unknown bounds): tile 0 sets the shift to the row max; a later tile rescales O and the row sum
+//          (and moves the shift) only for a row whose max exceeds the shift by more than kLazy (24), so P <= 2^24 and
+//          the row's largest term >= 1. Per tile: 16 v_max3 per lane and one ballot; the row reduction (two row swaps)
+//          and the rescale run only when a lane's own tile max crosses the threshold (rare after tile 0; rows below it
+//          take the branch with d = 0, exactly, so rows stay independent of each other).
+// The host picks the mode from the bounds (m16_mode).
 constexpr int kKStride16 = 288;
 constexpr int kVStride16 = 288;
 constexpr int kAhead = 3;  // MFMA phase: operand pairs read ahead of their MFMAs
@@ -121,7 +125,7 @@ constexpr int kKBuf16 = kKBlk * kKStride16;        // 18432
 constexpr int kVBuf16 = kKBlk * kVStride16;        // 18432
 constexpr int kLds16 = 2 * kKBuf16 + 2 * kVBuf16;  // 73728
 
-// kMode: 0 fixed shift, 1 fixed shift known to be 0 (pre-scaled q, bound product <= 60: no initial C), 2 online
+// kMode: 0 fixed shift, 1 fixed shift known to be 0 (pre-scaled q, bound product <= 96: no initial C), 2 online
 template <int kKind, bool kPre, int kMode>
 __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[kLds16];
@@ -170,7 +174,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
   typedef short s16x8v __attribute__((ext_vector_type(8)));
   const bf16x8 ones8 = __builtin_bit_cast(bf16x8, s16x8v{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80});
 
-  // ---- the rows' softmax shifts: fixed from |q_row| and the key bound (the host checked b_row <= 80), or online ----
+  // ---- the rows' softmax shifts: fixed from |q_row| and the key bound (the host checked b_row <= 98), or online ----
   const float cs = kPre ? 1.f : a.scale_log2;  // score -> log2 units
   float m_run[2] = {0.f, 0.f};
   if constexpr (kMode == 0) {
@@ -267,16 +271,17 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
     asm volatile("" : "+v"(S[0][0]), "+v"(S[0][1]), "+v"(S[1][0]), "+v"(S[1][1]), "+v"(S[2][0]), "+v"(S[2][1]),
                  "+v"(S[3][0]), "+v"(S[3][1]));
     if constexpr (online) {
-      float mx[2];
+      float mx[2];  // this lane's part of each row's tile max, above the row's current shift
 #pragma unroll
       for (int qh = 0; qh < 2; ++qh) {
         float x = fmaxf(S[0][qh][0], S[0][qh][1]);
 #pragma unroll
         for (int i = 2; i < 16; i += 2) x = fmaxf(fmaxf(x, S[i >> 2][qh][i & 3]), S[(i + 1) >> 2][qh][(i + 1) & 3]);
-        x = group4_max(x);
-        mx[qh] = kPre ? x : fmaf(x, cs, -m_run[qh]);  // the row's tile max above its current shift
+        mx[qh] = kPre ? x : fmaf(x, cs, -m_run[qh]);
       }
       if (__builtin_expect(t == 0 || __any(fmaxf(mx[0], mx[1]) > kLazy), 0)) {
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) mx[qh] = group4_max(mx[qh]);  // the whole row's (the shift is per row)
 #pragma unroll
         for (int qh = 0; qh < 2; ++qh) {
           // tile 0: the shift becomes the row max (O and the sum are still zero); later: only a row past the lazy
@@ -473,7 +478,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
 //   kF8 = 1 (cp25_attn_fwd_prescaled_fp8qk): q and k arrive as OCP e4m3 bytes (strides in bytes); Q K^T is 4 MFMAs of
 //     64 k per tile instead of 16 of 16, K tiles of 64 rows x 128 B (LDS rows 144 B). The operands' k order only has
 //     to agree between A and B: lane half h, byte i of both is d = 64 s + 32 h + i. P and V bf16 (V^T by
-//     ds_read_b64_tr_b16 from 320-B LDS rows), P = exp2(S) with no shift (host: |q| |k| <= 60).
+//     ds_read_b64_tr_b16 from 320-B LDS rows), P = exp2(S) with no shift (host: |q| |k| <= kTopF8 = 60).
 //   kF8 = 3 (cp25_attn_fwd_prescaled_fp8): also O^T += V^T P^T on fp8: P^T as e5m2 bytes straight from the S^T
 //     accumulator (byte j = 16 kt + r) made without exp2 (n = round(4 (S - shift) + 60) clamped to [0, 255] by one
 //     v_cvt_pk_u8_f32 after one fma is read as e5m2, i.e. 2^(n / 4 - 15) with a linear mantissa), V^T as e4m3 from
@@ -482,7 +487,6 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
 //     the P actually used). The shift keeps P <= 2^15 and enters as the Q K^T chains' initial C; the host runs this
 //     form only while the shift leaves the window [2^-15, 2^15] room for every row (1.13 |q| |k| <= 30), and a row
 //     whose every term still underflowed writes zeros (split: an empty partial), never NaN.
-constexpr int kKStride = 272;
 constexpr int kVStride = 320;
 constexpr int kVBuf = kKBlk * kVStride;  // 20480
 constexpr int kLdsF8 = 2 * kVBuf + 2 * kKBlk * 144;
@@ -870,7 +874,7 @@ int plan_split(int B, int H, int Lq, int Lk) {
 }
 
 // The m16 softmax-shift mode for these bounds (the bound product in log2 units; |q_row| <= q_norm_bound): 1 zero
-// shift (pre-scaled q, product <= 60), 0 fixed per-row shift (product <= 80), 2 online max (larger or unknown)
+// shift (pre-scaled q, product <= 96), 0 fixed per-row shift (product <= 98), 2 online max (larger or unknown)
 int m16_mode(float q_norm_bound, float k_norm_bound, float scale_log2, bool prescaled) {
   const double bb = (double)q_norm_bound * k_norm_bound * (prescaled ? 1.0 : scale_log2);
   if (!(q_norm_bound > 0.f && k_norm_bound > 0.f) || bb > kMaxBound) return 2;
@@ -890,7 +894,7 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
   if (fp8qk && !prescaled) return CP25_ERR_INVAL;
   if (fp8 == 2 && (!v_amax || ((uintptr_t)v_amax & 3))) return CP25_ERR_INVAL;
   // fp8 Q K^T: P = exp2(S) with no shift needs every score inside [-60, 60]
-  if (fp8qk && !(q_norm_bound > 0.f && k_norm_bound > 0.f && (double)q_norm_bound * k_norm_bound <= (double)kTop))
+  if (fp8qk && !(q_norm_bound > 0.f && k_norm_bound > 0.f && (double)q_norm_bound * k_norm_bound <= (double)kTopF8))
     return CP25_ERR_INVAL;
   // fp8 P.V: the e5m2 window [2^-15, 2^15] must hold a term of every row (shift 1.13 qb kb - 15 <= 15)
   if (fp8 == 2 && 1.13 * (double)q_norm_bound * k_norm_bound > 30.0) return CP25_ERR_INVAL;

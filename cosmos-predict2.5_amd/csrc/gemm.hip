@@ -231,15 +231,25 @@ constexpr int kBuf8 = 4 * kHalf;      // A0 A1 B0 B1
 // combined before the stores.
 // (Round-2 A/B variants of this kernel -- skipped / nontemporal stores, the lab switches -- are in git history,
 // DESIGN.md §3 "GEMM".)
-template <int kEpi>
+// kES = 1 (cp25_gemm_fp8, config 5's fp8 option): A and W are OCP e4m3 bytes with a per-row scale of A and a per-row
+// (output column) scale of W; a K-tile is 128 elements = the same 128-byte LDS rows, DMA pieces and fragment reads as
+// the bf16 tile, and each (i, j) of a phase is ONE v_mfma_scale_f32_16x16x128_f8f6f4 over the lane's two 16-B chunks
+// (k bytes 16 g .. and 64 + 16 g ..: the same k slots in A and B, which is all the sum needs) instead of two bf16
+// MFMAs: twice the cycles each, half the count, twice the K -- 2x the bf16 rate. The epilogue multiplies each
+// accumulator by a_scale[row] * w_scale[col] before the bf16 rounding (torch._scaled_mm's definition).
+template <int kEpi, int kES = 2>
 __global__ void __launch_bounds__(kThreads, 1)
 gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned short* __restrict__ W, int64_t ldw,
-            unsigned short* __restrict__ C, int64_t ldc, int M, int N, int K, ResEpi re) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf8];
+            unsigned short* __restrict__ C, int64_t ldc, int M, int N, int K, ResEpi re, const float* __restrict__ a_scale,
+            const float* __restrict__ w_scale) {
+  // fp8: 2 KiB past the K-tile buffers / C tile hold the tile's 256 row scales of A and 256 column scales of W
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf8 + (kES == 1 ? 2048 : 0)];
+  static_assert(kES == 1 || kES == 2, "bf16 (2) or fp8 (1) operands");
+  typedef int i32x8 __attribute__((ext_vector_type(8)));
 
   const int mt = (M + kBM - 1) / kBM, nt = N / kBN;
   const int n_tiles = mt * nt;
-  const int nk = K / kBK;
+  const int nk = K * kES / (kBK * 2);  // 128-byte K-tiles
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -263,16 +273,16 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int c = ppos ^ ((4 * j + (prow >> 1)) & 7);  // r = (2 wave + j) 8 + prow: (r >> 1) & 7 = (4 j + prow / 2) & 7
-    w_vo[j] = prow * (int)ldw * 2 + c * 16;
+    w_vo[j] = prow * (int)ldw * kES + c * 16;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) a_vo[h][j] = ((2 * wave + j) * 8 + h * 128 + prow) * (int)lda * 2 + c * 16;
+    for (int h = 0; h < 2; ++h) a_vo[h][j] = ((2 * wave + j) * 8 + h * 128 + prow) * (int)lda * kES + c * 16;
   }
   __amdgpu_buffer_rsrc_t a_rsrc, w_rsrc;
   auto set_tile = [&](int m0, int n0) __attribute__((always_inline)) {
-    a_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (int64_t)m0 * lda), (short)0,
-                                               (int)((int64_t)min(M - m0, kBM) * lda * 2), 0x00020000);
-    w_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(W + (int64_t)n0 * ldw), (short)0, (int)((int64_t)kBN * ldw * 2),
-                                               0x00020000);
+    a_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)A + (int64_t)m0 * lda * kES), (short)0,
+                                               (int)((int64_t)min(M - m0, kBM) * lda * kES), 0x00020000);
+    w_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)W + (int64_t)n0 * ldw * kES), (short)0,
+                                               (int)((int64_t)kBN * ldw * kES), 0x00020000);
   };
   // part 0: B half 0, 1: A half 0, 2: B half 1, 3: A half 1 (LDS: A0 @0, A1 @16K, B0 @32K, B1 @48K)
   auto issue = [&](int part, int kt, int buf) __attribute__((always_inline)) {
@@ -284,7 +294,19 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
       if (is_a)
         dma16(a_rsrc, (lds_void_ptr)(dst + j * 1024), a_vo[h][j], kt * kBK * 2);
       else
-        dma16(w_rsrc, (lds_void_ptr)(dst + j * 1024), w_vo[j], ((2 * wave + j) * 8 + h * 128) * (int)ldw * 2 + kt * kBK * 2);
+        dma16(w_rsrc, (lds_void_ptr)(dst + j * 1024), w_vo[j], ((2 * wave + j) * 8 + h * 128) * (int)ldw * kES + kt * kBK * 2);
+    }
+  };
+  // fp8: the tile's scales ride the DMA queue ahead of K-tile 0 (one dword per lane: waves 0-3 the 256 row scales of
+  // A -- rows past M read 0 from the descriptor bound --, waves 4-7 the 256 column scales of W), so the epilogue
+  // reads them from the LDS instead of paying a global-load round trip per tile. Retired with K-tile 0.
+  auto issue_scales = [&](int m0, int n0) __attribute__((always_inline)) {
+    if constexpr (kES == 1) {
+      const bool is_a = wave < 4;
+      const __amdgpu_buffer_rsrc_t s_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(is_a ? a_scale + m0 : w_scale + n0), (short)0, is_a ? min(M - m0, kBM) * 4 : kBN * 4, 0x00020000);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(s_rsrc, (lds_void_ptr)(smem + 2 * kBuf8 + wave * 256), 4,
+                                               ((wave & 3) * 64 + lane) * 4, 0, 0, 0);  // bound-checked offset
     }
   };
   auto issue_first_two = [&]() __attribute__((always_inline)) {  // K-tiles 0 and 1 of a tile (nk is even)
@@ -348,13 +370,26 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
     __builtin_amdgcn_s_setprio(1);
     constexpr int mq = Q >> 1, nq = (Q == 1 || Q == 2);
     auto& fb = nq ? fb1 : fb0;
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
+    if constexpr (kES == 1) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[mq][nq][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb[j][s], acc[mq][nq][i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) {
+          const u32x4 a0 = __builtin_bit_cast(u32x4, fa[i][0]), a1 = __builtin_bit_cast(u32x4, fa[i][1]);
+          const u32x4 b0 = __builtin_bit_cast(u32x4, fb[j][0]), b1 = __builtin_bit_cast(u32x4, fb[j][1]);
+          const i32x8 av = {(int)a0[0], (int)a0[1], (int)a0[2], (int)a0[3], (int)a1[0], (int)a1[1], (int)a1[2], (int)a1[3]};
+          const i32x8 bv = {(int)b0[0], (int)b0[1], (int)b0[2], (int)b0[3], (int)b1[0], (int)b1[1], (int)b1[2], (int)b1[3]};
+          acc[mq][nq][i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, bv, acc[mq][nq][i][j], 0, 0, 0, 0, 0, 0);
+        }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[mq][nq][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb[j][s], acc[mq][nq][i][j], 0, 0, 0);
+    }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
@@ -366,8 +401,9 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
   int m0, n0;
   tile_mn(tile, m0, n0);
   set_tile(m0, n0);
+  issue_scales(m0, n0);
   issue_first_two();
-  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // K-tile 0
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // K-tile 0 (and the fp8 scales)
   __builtin_amdgcn_s_barrier();
 
   using I0 = std::integral_constant<int, 0>;
@@ -426,7 +462,13 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
           for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              float y = rbf(acc[mq][nq][i][j][r]);
+              float a = acc[mq][nq][i][j][r];
+              if constexpr (kES == 1) {  // row mq 128 + wr 64 + 16 i + 4 fg + r, column nq 128 + wc 32 + 16 j + fr
+                const float* sc = reinterpret_cast<const float*>(smem + 2 * kBuf8) + ez;
+                const f32x4_t as = *reinterpret_cast<const f32x4_t*>(sc + mq * 128 + wr * 64 + 16 * i + 4 * fg);
+                a = a * as[r] * sc[256 + nq * 128 + wc * 32 + 16 * j + fr];
+              }
+              float y = rbf(a);
               if constexpr (kEpi == CP25_EPI_GELU) y = gelu_exact(y);
               stj[j][(mq * 128 + 16 * i + r) * 256 + nq * 128] = f2bf(y);
             }
@@ -478,6 +520,7 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
       tile = next;
       tile_mn(tile, m0, n0);
       set_tile(m0, n0);
+      issue_scales(m0, n0);
       issue_first_two();
     }
     __builtin_amdgcn_sched_barrier(0);  // the DMAs are queued ahead of the stores (the counts above rely on it)
@@ -542,17 +585,70 @@ static int gemm_launch(const void* a, int64_t lda, const void* w, int64_t ldw, v
   } else {
     switch (epilogue) {
       case CP25_EPI_GELU:
-        hipLaunchKernelGGL(gemm_nt_8ph<CP25_EPI_GELU>, pgrid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re);
+        hipLaunchKernelGGL((gemm_nt_8ph<CP25_EPI_GELU, 2>), pgrid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re,
+                           nullptr, nullptr);
         break;
       case CP25_EPI_RES:
-        hipLaunchKernelGGL(gemm_nt_8ph<CP25_EPI_RES>, pgrid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re);
+        hipLaunchKernelGGL((gemm_nt_8ph<CP25_EPI_RES, 2>), pgrid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re,
+                           nullptr, nullptr);
         break;
       default:
-        hipLaunchKernelGGL(gemm_nt_8ph<CP25_EPI_NONE>, pgrid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re);
+        hipLaunchKernelGGL((gemm_nt_8ph<CP25_EPI_NONE, 2>), pgrid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re,
+                           nullptr, nullptr);
     }
   }
   CP25_LAUNCH_CHECK();
   return CP25_OK;
+}
+
+static int gemm_fp8_launch(const void* a, int64_t lda, const float* a_scale, const void* w, int64_t ldw,
+                           const float* w_scale, void* c, int64_t ldc, int M, int N, int K, int epilogue,
+                           const ResEpi& re, hipStream_t stream) {
+  if (!a || !w || !c || !a_scale || !w_scale || M <= 0 || N <= 0 || K <= 0) return CP25_ERR_INVAL;
+  if (N % kBN != 0 || K % 256 != 0) return CP25_ERR_DTYPE;  // 256-wide output tiles, an even number of 128-deep K-tiles
+  if (lda < K || ldw < K || ldc < N || (lda % 16) || (ldw % 16) || (ldc % 8)) return CP25_ERR_INVAL;
+  if (lda >= (1 << 23) || ldw >= (1 << 23)) return CP25_ERR_INVAL;
+  if (((uintptr_t)a | (uintptr_t)w | (uintptr_t)c) & 15 || ((uintptr_t)a_scale | (uintptr_t)w_scale) & 3)
+    return CP25_ERR_INVAL;
+  if (epilogue != CP25_EPI_NONE && epilogue != CP25_EPI_RES) return CP25_ERR_INVAL;
+  if (epilogue == CP25_EPI_RES &&
+      (!re.x || !re.gate || re.B <= 0 || 16 % re.B || re.hw < 16 / re.B || re.tok0 < 0 || (re.x_st % 8) ||
+       (re.x_sb % 8) || (re.g_sb % 8) || (re.g_st % 8) || (((uintptr_t)re.x | (uintptr_t)re.gate) & 15)))
+    return CP25_ERR_INVAL;
+  const int64_t nwg = (int64_t)((M + kBM - 1) / kBM) * (N / kBN);
+  if (nwg > 0x7fffffff) return CP25_ERR_INVAL;
+  static int n_cu[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return CP25_ERR_LAUNCH;
+  if (!n_cu[dev] && hipDeviceGetAttribute(&n_cu[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return CP25_ERR_LAUNCH;
+  const int cus = n_cu[dev] >= 8 ? n_cu[dev] & ~7 : n_cu[dev];
+  const dim3 pgrid((unsigned)std::min<int64_t>(nwg, cus)), block(kThreads);
+  auto* A = (const unsigned short*)a;
+  auto* Wp = (const unsigned short*)w;
+  auto* Cp = (unsigned short*)c;
+  if (epilogue == CP25_EPI_RES)
+    hipLaunchKernelGGL((gemm_nt_8ph<CP25_EPI_RES, 1>), pgrid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re,
+                       a_scale, w_scale);
+  else
+    hipLaunchKernelGGL((gemm_nt_8ph<CP25_EPI_NONE, 1>), pgrid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re,
+                       a_scale, w_scale);
+  CP25_LAUNCH_CHECK();
+  return CP25_OK;
+}
+
+extern "C" int cp25_gemm_fp8(const void* a, int64_t lda, const float* a_scale, const void* w, int64_t ldw,
+                             const float* w_scale, void* c, int64_t ldc, int M, int N, int K, hipStream_t stream) {
+  const ResEpi re{};
+  return gemm_fp8_launch(a, lda, a_scale, w, ldw, w_scale, c, ldc, M, N, K, CP25_EPI_NONE, re, stream);
+}
+
+extern "C" int cp25_gemm_fp8_res(const void* a, int64_t lda, const float* a_scale, const void* w, int64_t ldw,
+                                 const float* w_scale, void* c, int64_t ldc, int M, int N, int K, const void* x,
+                                 int64_t x_st, int64_t x_sb, const void* gate, int64_t g_sb, int64_t g_st, int B,
+                                 int64_t tok0, int64_t hw, hipStream_t stream) {
+  const ResEpi re{(const unsigned short*)x, x_st, x_sb, (const unsigned short*)gate, g_sb, g_st, B, tok0, hw};
+  return gemm_fp8_launch(a, lda, a_scale, w, ldw, w_scale, c, ldc, M, N, K, CP25_EPI_RES, re, stream);
 }
 
 extern "C" int cp25_gemm_epi(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int M,

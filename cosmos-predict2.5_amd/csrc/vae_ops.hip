@@ -596,6 +596,13 @@ __global__ void __launch_bounds__(256) softmax_rows_kernel(const float* __restri
 
 }  // namespace
 
+// conv kernel selection, set once at library load from CP25_CONV_KERNEL ("tap": the per-tap kernel only) and
+// changed only through cp25_conv3d_select (never read from the environment per launch)
+static int g_conv_select = [] {
+  const char* e = std::getenv("CP25_CONV_KERNEL");
+  return (e && !std::strcmp(e, "tap")) ? 1 : 0;
+}();
+
 extern "C" int cp25_conv3d(const void* const* frames, int n_frames, const void* weight, const void* bias,
                            const void* residual, void* out, int Hin, int Win, int Cin, int Cout, int Tout, int KT,
                            int KH, int KW, int stride_t, int stride_hw, int pad_top, int pad_left, int pad_bottom,
@@ -621,13 +628,12 @@ extern "C" int cp25_conv3d(const void* const* frames, int n_frames, const void* 
   a.out_split = out_split;
   a.out_C = out_split > 0 ? out_split : Cout;
   if (a.Ho <= 0 || a.Wo <= 0) return CP25_ERR_INVAL;
-  // 3x3 stride-1 pad-1 convs: the halo kernel (CP25_CONV_KERNEL=tap selects the per-tap kernel, A/B only)
-  const char* sel = std::getenv("CP25_CONV_KERNEL");
+  // 3x3 stride-1 pad-1 convs: the halo kernel (cp25_conv3d_select(1) selects the per-tap kernel, A/B and tests)
   // (any top / bottom pad: the banded decode passes haloed bands with pads 0 or -1 there)
   const bool halo_ok = KH == 3 && KW == 3 && stride_hw == 1 && out_split == 0 && pad_left == 1 && pad_right == 1 &&
                        Cout >= 64 && KT <= 3 && a.Wo % 32 == 0 &&
                        (int64_t)Hin * Win * Cin < (1LL << 31) && (int64_t)Cout * KT * 9 * Cin < (1LL << 31) &&
-                       !(sel && !std::strcmp(sel, "tap"));
+                       g_conv_select == 0;
   if (halo_ok) {
     const int tw = a.Wo % 128 == 0 ? 128 : (a.Wo % 64 == 0 ? 64 : 32);
     // BN = 96 for every Cout (96 / 192 / 384 in the decoder): with BN = 128 the 256 accumulators spill
@@ -647,6 +653,13 @@ extern "C" int cp25_conv3d(const void* const* frames, int n_frames, const void* 
   CONV_CASE(64, 1) CONV_CASE(64, 2) CONV_CASE(64, 3) CONV_CASE(64, 4)
 #undef CONV_CASE
   return CP25_ERR_DTYPE;
+}
+
+extern "C" int cp25_conv3d_select(int mode) {
+  if (mode < 0 || mode > 1) return CP25_ERR_INVAL;
+  const int prev = g_conv_select;
+  g_conv_select = mode;
+  return prev;
 }
 
 extern "C" int cp25_softmax_rows(const float* s, int64_t rows, int cols, int64_t ld_s, float scale, void* p,

@@ -52,11 +52,11 @@ int cp25_attn_fwd_split(const void* q, const void* k, const void* v, void* o, in
 /* cp25_attn_fwd_split with caller-supplied upper bounds of the query and key norms:
  * q_norm_bound >= max |q| and k_norm_bound >= max |k| over all rows (0 = unknown). Softmax is shift invariant, so a
  * row's shift only has to keep its terms inside the fp32 / bf16 range. When both bounds are given and
- * b = q_norm_bound * k_norm_bound * softmax_scale * log2(e) <= 80, every score of a row lies in [-b_row, b_row]
- * (Cauchy-Schwarz, b_row from the row's own |q|) and the row uses the fixed shift max(b_row - 60, 0): no max
- * reduction and no output rescale per key tile, every term within [2^-100, 2^60]. Otherwise (or with a 0 bound) the
+ * b = q_norm_bound * k_norm_bound * softmax_scale * log2(e) <= 98, every score of a row lies in [-b_row, b_row]
+ * (Cauchy-Schwarz, b_row from the row's own |q|) and the row uses the fixed shift max(b_row - 96, 0): no max
+ * reduction and no output rescale per key tile, the row's largest term >= 2^-100 and every term <= 2^96. Otherwise (or with a 0 bound) the
  * rows run an online max (tile 0 sets the shift to the row max; later tiles move it up, rescaling O and the sum, only
- * when a row max exceeds it by more than 8): any data. Same result as cp25_attn_fwd_split up to rounding. The DiT
+ * when a row max exceeds it by more than 24): any data. Same result as cp25_attn_fwd_split up to rounding. The DiT
  * passes sqrt(D) * max|q_norm.weight| and sqrt(D) * max|k_norm.weight|: the q/k RMSNorm (minimal_v4_dit.py:355-358)
  * bounds every normed row by them and RoPE preserves the norm. */
 int cp25_attn_fwd_bounded(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq, int Lk,
@@ -67,7 +67,7 @@ int cp25_attn_fwd_bounded(const void* q, const void* k, const void* v, void* o, 
 /* cp25_attn_fwd_bounded over a PRE-SCALED q (rows already multiplied by softmax_scale * log2(e), e.g. by
  * cp25_head_rmsnorm_rope_scaled): P = exp2(q k^T - shift) with the row's shift as the initial accumulator of its
  * Q K^T MFMA chains, so no per-score multiply or subtract. Bounds (of the scaled q and of k; 0 = unknown) pick the
- * shift as in cp25_attn_fwd_bounded: product <= 60 no shift, <= 80 a fixed per-row shift, else the online max.
+ * shift as in cp25_attn_fwd_bounded: product <= 96 no shift, <= 98 a fixed per-row shift, else the online max.
  * Rounds q * scale to bf16 instead of q (the same single bf16 rounding of the query). Replaces the same reference
  * code as cp25_attn_fwd_bounded; the DiT's default form. */
 int cp25_attn_fwd_prescaled(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq, int Lk, int D,
@@ -207,6 +207,20 @@ int cp25_gemm_res(const void* a, int64_t lda, const void* w, int64_t ldw, void* 
                   const void* x, int64_t x_st, int64_t x_sb, const void* gate, int64_t g_sb, int64_t g_st, int B,
                   int64_t tok0, int64_t hw, hipStream_t stream);
 
+/* The config-5 fp8 option's block projections on the same hand-written GEMM (no reference counterpart: the reference
+ * has no fp8 path): C[M, N] = bf16((A[M, K] W[N, K]^T) * a_scale[m] * w_scale[n]) with A and W OCP e4m3 bytes
+ * (row-scaled activations from cp25_ln_mod_fp8 / cp25_quant_fp8_rows / cp25_gelu_quant_fp8; per-output-channel weight
+ * scales), fp32 accumulation on v_mfma_scale_f32_16x16x128_f8f6f4 -- torch._scaled_mm's definition with row / column
+ * scales. N % 256 == 0, K % 256 == 0 (-95 otherwise), lda / ldw multiples of 16 bytes, any M. cp25_gemm_fp8_res adds
+ * cp25_gemm_res's gated-residual epilogue (same x / gate arguments).
+ * Replaces: the block nn.Linear layers of minimal_v4_dit.py (:400-432, :227-254) in the fp8 option. */
+int cp25_gemm_fp8(const void* a, int64_t lda, const float* a_scale, const void* w, int64_t ldw, const float* w_scale,
+                  void* c, int64_t ldc, int M, int N, int K, hipStream_t stream);
+int cp25_gemm_fp8_res(const void* a, int64_t lda, const float* a_scale, const void* w, int64_t ldw,
+                      const float* w_scale, void* c, int64_t ldc, int M, int N, int K, const void* x, int64_t x_st,
+                      int64_t x_sb, const void* gate, int64_t g_sb, int64_t g_st, int B, int64_t tok0, int64_t hw,
+                      hipStream_t stream);
+
 /* Latents live in "patch layout" [n_tok, 64] fp32, element (tok, p*16 + c), p = p1*2 + p2 (the
  * final layer's "(p1 p2 t C)" order). cp25_patchify builds the x_embedder input rows [n_tok, 72]
  * bf16 (feature c*4 + p): channels 0..15 = gt*mask + x*(1-mask) (gt may be NULL), channel 16 = the
@@ -261,6 +275,11 @@ int cp25_conv3d(const void* const* frames, int n_frames, const void* weight, con
                 void* out, int Hin, int Win, int Cin, int Cout, int Tout, int KT, int KH, int KW, int stride_t,
                 int stride_hw, int pad_top, int pad_left, int pad_bottom, int pad_right, int upsample, int out_split,
                 hipStream_t stream);
+
+/* Kernel choice of cp25_conv3d for the 3x3 stride-1 convs: 0 (default) the LDS-halo kernel where it applies, 1 the
+ * per-tap implicit GEMM everywhere (A/B runs and tests; same arithmetic up to summation order). Returns the previous
+ * mode. The initial mode is read once at library load from CP25_CONV_KERNEL ("tap" = 1). */
+int cp25_conv3d_select(int mode);
 
 /* y = F.normalize(x, dim=C) * sqrt(C) * gamma [then SiLU] per pixel of n_pix channels-last pixels,
  * with the reference's bf16 rounding after each torch op. C % 32 == 0, C/32 in {1,2,3,6,12}.

@@ -253,8 +253,9 @@ def encode(sd, video: torch.Tensor, temporal_window: int = 16) -> torch.Tensor:
     return (mu - mean.view(1, 16, 1, 1, 1)) * inv_std.view(1, 16, 1, 1, 1)
 
 
-def decode(sd, z: torch.Tensor) -> torch.Tensor:
-    """latent [B, 16, T, h, w] -> video [B, 3, 1 + 4 (T-1), 8h, 8w] (bf16, ~[-1, 1])."""
+def decode(sd, z: torch.Tensor, progress=None) -> torch.Tensor:
+    """latent [B, 16, T, h, w] -> video [B, 3, 1 + 4 (T-1), 8h, 8w] (bf16, ~[-1, 1]). progress(i): called after each
+    latent frame (long runs report liveness)."""
     mean, inv_std = _scale(z.device)
     z = z.to(act_dtype())
     z = z / inv_std.view(1, 16, 1, 1, 1) + mean.view(1, 16, 1, 1, 1)
@@ -264,4 +265,6 @@ def decode(sd, z: torch.Tensor) -> torch.Tensor:
     for i in range(z.shape[2]):
         cache.reset_idx()
         outs.append(decoder3d(sd, x[:, :, i: i + 1], cache))
+        if progress is not None:
+            progress(i)
     return torch.cat(outs, 2)

@@ -5,9 +5,9 @@ Reference op: networks/attention.py:90-181 (softmax(q k^T / sqrt(D)) v, bf16 ope
 tests/test_attention_gpu.py (rel-L2 <= 4e-3 vs fp32: P rounded to bf16 before P.V, bf16 output). The modes differ
 only in the shift at which P is rounded to bf16, so two modes agree within two independent roundings (1.5 x TOL).
 Modes (the library picks one from the norm bounds, attn_fwd.hip):
-  fixed  norm bounds with max|q| max|k| <= 80 (log2 units): per-row shift max(|q_row| max|k| - 60, 0);
-  zero   pre-scaled q and bound product <= 60: no shift at all (the round-2 prescaled kernel);
-  online no bounds or a larger product: the row max of tile 0, moved up lazily (> 8 above the shift).
+  fixed  norm bounds with max|q| max|k| <= 98 (log2 units): per-row shift max(|q_row| max|k| - 96, 0);
+  zero   pre-scaled q and bound product <= 96: no shift at all (the round-2 prescaled kernel);
+  online no bounds or a larger product: the row max of tile 0, moved up lazily (> 24 above the shift).
 """
 import pytest
 import torch
@@ -63,8 +63,8 @@ def test_m16_modes_match_fp32(device, B, H, Lq, Lk, n_split, prescaled):
         ref = ref_attention(qin, k, v, 1.0 / LOG2E)
         base = dict(prescaled=True, n_split=n_split)
         qb = qin.float().norm(dim=-1).max().item() * 1.01
-        # zero shift (product <= 60), fixed shift (product in (60, 80]: inflated q bound), online
-        modes = {"zero": dict(base, norm_bounds=(qb, kn)), "fixed": dict(base, norm_bounds=(70.0 / kn, kn)),
+        # zero shift (product <= 96), fixed shift (product in (96, 98]: inflated q bound), online
+        modes = {"zero": dict(base, norm_bounds=(qb, kn)), "fixed": dict(base, norm_bounds=(97.0 / kn, kn)),
                  "online": dict(base)}
     else:
         qin = q
@@ -97,11 +97,13 @@ def test_m16_strided_token_major_views(device):
         assert rel_l2(out.transpose(0, 1), ref) <= TOL
 
 
-def test_m16_fixed_extremes_and_guard(device):
-    """Fixed mode: rows whose every score sits at +b or -b (b = 78 log2 units: terms 2^60 and 2^-96) still average
-    V; a norm bound far below the real norms poisons the rows (non-finite) instead of a silent wrong answer."""
+@pytest.mark.parametrize("bound", [78.0, 97.5])
+def test_m16_fixed_extremes_and_guard(device, bound):
+    """Fixed mode: rows whose every score sits at +b or -b (b = 78: terms 2^78 and 2^-78, no shift; b = 97.5: shift
+    1.5, terms 2^96 and 2^-99) still average V; a norm bound far below the real norms poisons the rows (non-finite)
+    instead of a silent wrong answer."""
     g = torch.Generator(device="cpu").manual_seed(11)
-    r = (78.0 * 128 ** 0.5 / LOG2E) ** 0.5
+    r = (bound * 128 ** 0.5 / LOG2E) ** 0.5
     u = torch.randn(128, generator=g)
     u = u / u.norm() * r * 0.999
     q = torch.randn(1, 64, 1, 128, generator=g)

@@ -119,7 +119,8 @@ def _case():
 
 
 def _worker(rank, world, port, q_out):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), CP25_ATTN_SPLIT="1")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    N.set_attn_split(1)  # no key split: rows equal to the single-rank run bit for bit
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from cosmos_predict2.attn_op import CP25AttnOp

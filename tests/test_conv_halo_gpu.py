@@ -1,5 +1,5 @@
 """The 3x3 halo conv (conv3x3_halo_kernel: LDS halo tile per (temporal tap, 16-channel chunk), the 9 spatial taps
-read from it) vs fp32 math and vs the per-tap implicit-GEMM kernel (CP25_CONV_KERNEL=tap).
+read from it) vs fp32 math and vs the per-tap implicit-GEMM kernel (cp25_conv3d_select(1)).
 
 Reference: CausalConv3d (tokenizers/wan2pt1.py:44-62) and the Resample upsample conv (:96-110). The halo
 kernel sums the same products in another order (channel chunk outer, tap inner), so it is held to the
@@ -7,12 +7,11 @@ single-conv bound vs fp32 (rel-L2 <= 2e-3, one bf16 output rounding) and to <= 2
 Shapes cover the three tile widths (Wo % 128, % 64, % 32), a ragged last row-tile, a causal zero frame, the
 nearest-2x upsample gather, bias + residual, and Cout = 192 / 384 (several 96-channel tiles).
 """
-import os
-
 import pytest
 import torch
 import torch.nn.functional as F
 
+from cosmos_predict2 import _native as N
 from cosmos_predict2.vae import _Conv
 
 pytestmark = pytest.mark.gpu
@@ -24,11 +23,11 @@ def _rel(a, b):
 
 def _both(fn):
     out = fn()
-    os.environ["CP25_CONV_KERNEL"] = "tap"
+    prev = N.conv3d_select(1)
     try:
         ref = fn()
     finally:
-        os.environ.pop("CP25_CONV_KERNEL")
+        N.conv3d_select(prev)
     return out, ref
 
 

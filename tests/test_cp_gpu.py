@@ -69,8 +69,7 @@ def _set_precision(m, precision):
 
 def _worker(rank, world, port, q, split_env, precision="bf16"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    if split_env:
-        os.environ["CP25_ATTN_SPLIT"] = split_env
+    N.set_attn_split(int(split_env) if split_env else None)  # _native was imported with this module, before any env
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from cosmos_predict2.model import Video2WorldModelRectifiedFlow

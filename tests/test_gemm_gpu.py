@@ -81,3 +81,37 @@ def test_gemm_residual_epilogue(device, M, Nn, K, B, hw, tok0, xsb0):
     assert torch.equal(out.view(n_tok, B, Nn).float(), ref)
     with pytest.raises(ValueError):
         N.gemm_res(a, w, x, x.stride(0), 0, gate[:, :1], B=B, tok0=tok0 + hw * T, hw=hw)  # frames past the gate
+
+
+@pytest.mark.parametrize("M,Nn,K", [(1000, 256, 512), (2048, 2048, 2048), (515, 6144, 2048), (4352, 2048, 8192),
+                                    (777, 8192, 2048)])
+def test_gemm_fp8_matches_dequantised(device, M, Nn, K):
+    """cp25_gemm_fp8 (config 5's fp8 option; the reference has no fp8 path): bf16((q w8^T) * s_row * s_col) on
+    v_mfma_scale_f32_16x16x128_f8f6f4 against the same product in fp32 on the dequantised operands (one bf16 output
+    rounding, rel-L2 <= 4e-3) and against torch._scaled_mm (hipBLASLt) on the same operands; rows independent of M;
+    the residual epilogue bit-exact vs x + gate * y on the kernel's own product."""
+    g = torch.Generator(device=device).manual_seed(M + Nn + K)
+    x = torch.randn(M, K, device=device, generator=g).to(torch.bfloat16)
+    w = (torch.randn(Nn, K, device=device, generator=g) * K ** -0.5).to(torch.bfloat16)
+    q, s = N.quant_fp8_rows(x)
+    fmax = torch.finfo(torch.float8_e4m3fn).max
+    ws = (w.float().abs().amax(1, keepdim=True) / fmax).clamp_min(1e-30)
+    w8 = (w.float() / ws).clamp(-fmax, fmax).to(torch.float8_e4m3fn)
+    wsr = ws.t().contiguous()
+    out = N.gemm_fp8(q, s, w8, wsr)
+    ref = (q.float() * s) @ (w8.float() * ws).t()
+    lib = torch._scaled_mm(q, w8.t(), scale_a=s, scale_b=wsr, out_dtype=torch.bfloat16)
+    e, el, d = _rel(out, ref), _rel(lib, ref), _rel(out, lib)
+    print(f"gemm fp8 M={M} N={Nn} K={K}: vs dequantised fp32 {e:.2e} (torch._scaled_mm {el:.2e}), own vs lib {d:.2e}")
+    assert torch.isfinite(out.float()).all()
+    assert e <= 4e-3, e
+    assert d <= 6e-3, d
+    m2 = M // 3 + 5
+    assert torch.equal(N.gemm_fp8(q[:m2].contiguous(), s[:m2].contiguous(), w8, wsr), out[:m2])
+    B, hw = 1, 64
+    gate = torch.randn(1, (M + hw - 1) // hw, Nn, device=device, generator=g).to(torch.bfloat16)
+    xr = torch.randn(M, 1, Nn, device=device, generator=g).to(torch.bfloat16)
+    o2 = N.gemm_fp8(q, s, w8, wsr, res=(xr, xr.stride(0), xr.stride(1), gate, B, 0, hw))
+    fr = torch.arange(M, device=device) // hw
+    exp = _rbf(xr[:, 0].float() + _rbf(gate[0, fr].float() * out.float()))
+    assert torch.equal(o2.float(), exp)

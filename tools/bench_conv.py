@@ -1,5 +1,5 @@
 """cp25_conv3d at the decoder's dominant shapes (704x1280 / 352x640 / 176x320, 3x3x3, 4 output frames): the halo
-kernel (default) vs the per-tap kernel (CP25_CONV_KERNEL=tap), HIP events, interleaved rounds in one process.
+kernel (default) vs the per-tap kernel (cp25_conv3d_select(1)), HIP events, interleaved rounds in one process.
 One JSON line per shape: ms and TFLOP/s (2 * 27 * Cin * Cout per output pixel)."""
 import json
 import os
@@ -10,6 +10,7 @@ sys.path.insert(0, os.path.join(ROOT, "cosmos-predict2.5_amd"))
 
 import torch  # noqa: E402
 
+from cosmos_predict2 import _native as N  # noqa: E402
 from cosmos_predict2.vae import _Conv  # noqa: E402
 
 dev = torch.device("cuda:0")
@@ -41,10 +42,9 @@ for i, (cin, cout, H, W) in enumerate(SHAPES):
     res = {"halo": [], "tap": []}
     for _ in range(int(os.environ.get("ROUNDS", "2"))):
         for k in ("halo", "tap"):
-            if k == "tap":
-                os.environ["CP25_CONV_KERNEL"] = "tap"
+            prev = N.conv3d_select(1 if k == "tap" else 0)
             res[k].append(timed(run))
-            os.environ.pop("CP25_CONV_KERNEL", None)
+            N.conv3d_select(prev)
     flop = 2.0 * 27 * cin * cout * H * W * 4
     rec = {"conv": f"{cin}->{cout} 3x3x3 {H}x{W} x4 frames", "halo_ms": min(res["halo"]), "tap_ms": min(res["tap"]),
            "halo_tflops": flop / min(res["halo"]) / 1e9, "tap_tflops": flop / min(res["tap"]) / 1e9}
