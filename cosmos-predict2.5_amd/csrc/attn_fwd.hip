@@ -459,6 +459,29 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
         *reinterpret_cast<f32x4*>(op + 16 * db) = w;
       }
       if (g == 0) a.lse_part[row] = m_run[qh] + __log2f(l_tot);
+    } else if constexpr (kKind == 1) {
+      // cross-attention (8 key tiles per workgroup, so the store tail counts): 16-B stores, 8 x 16 B per lane instead
+      // of 16 x 8 B (the tail is store-issue-bound, cdna_hip_programming T21; 1.278 -> 1.228 ms per launch, same box,
+      // profiles/r3/attn_epilogue_ab.log). For each pair of d blocks (2m, 2m + 1) the lane rows g and g ^ 1 (lanes
+      // l, l ^ 16) swap halves with one v_permlane16_swap per dword (odd rows of the first operand <-> even rows of
+      // the second), so an even-g lane holds d 32 m + 4 g .. + 8 of block 2m and an odd-g lane d 32 m + 16 +
+      // 4 (g - 1) .. + 8 of block 2m + 1. (The self-attention keeps the 8-B stores: with 1 705 key tiles per
+      // workgroup the tail is noise, and the 16-B form's register allocation measured 0.9 % slower there.)
+      const bool odd = g & 1;
+      unsigned short* op = a.o + b * a.o_sb + h * a.o_sh + (int64_t)q_row[qh] * a.o_sl + (odd ? 16 + 4 * (g - 1) : 4 * g);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        unsigned lo[2], hi[2];  // block 2m, block 2m + 1 (two packed bf16 pairs each)
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {
+          lo[w] = f2bf(o[2 * m][qh][2 * w] * inv) | ((unsigned)f2bf(o[2 * m][qh][2 * w + 1] * inv) << 16);
+          hi[w] = f2bf(o[2 * m + 1][qh][2 * w] * inv) | ((unsigned)f2bf(o[2 * m + 1][qh][2 * w + 1] * inv) << 16);
+          const auto r = __builtin_amdgcn_permlane16_swap(lo[w], hi[w], false, false);
+          lo[w] = r[0];
+          hi[w] = r[1];
+        }
+        *reinterpret_cast<u32x4*>(op + 32 * m) = u32x4{lo[0], lo[1], hi[0], hi[1]};
+      }
     } else {
       unsigned short* op = a.o + b * a.o_sb + h * a.o_sh + (int64_t)q_row[qh] * a.o_sl + 4 * g;
 #pragma unroll

@@ -3,7 +3,8 @@ CFG 2), HIP events, interleaved rounds in one process. One JSON line per shape:
   bf16: cp25_gemm_epi vs torch.matmul; MLP1 + GELU fused vs matmul + cp25_gelu; the gated residual fused
         (cp25_gemm_res, then the LN-mod reads x' only) vs matmul + cp25_ln_mod(x, y, gate);
   fp8 : cp25_gemm_fp8 vs torch._scaled_mm on the same row-scaled e4m3 operands (config 5's option).
-usage: python tools/bench_gemm.py [--rounds 2] [--fp8]"""
+usage: python tools/bench_gemm.py [--rounds 2] [--fp8] [--shapes qkv,mlp1] [--plain] [--lib tools/lab/libcp25_<x>.so]
+(--plain: own vs library only, no fused comparisons; --lib: a lab build, tools/lab/gemm_variant.py)"""
 import argparse
 import json
 import os
@@ -36,15 +37,22 @@ def main():
     ap.add_argument("--M", type=int, default=218240)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--fp8", action="store_true")
+    ap.add_argument("--shapes", default="qkv,proj,mlp1,mlp2")
+    ap.add_argument("--plain", action="store_true")
+    ap.add_argument("--lib", default="")
     a = ap.parse_args()
+    if a.lib:
+        N._LIB_PATH = a.lib
     M, B, hw, T = a.M, 2, 3520, 31
     for name, Nn, K in (("qkv", 6144, 2048), ("proj", 2048, 2048), ("mlp1", 8192, 2048), ("mlp2", 2048, 8192)):
+        if name not in a.shapes.split(","):
+            continue
         g = torch.Generator(device=dev).manual_seed(0)
         x = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
         w = (torch.randn(Nn, K, device=dev, generator=g) * K ** -0.5).to(torch.bfloat16)
         out = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
         flop = 2.0 * M * Nn * K
-        rec = {"gemm": name, "M": M, "N": Nn, "K": K}
+        rec = {"gemm": name, "M": M, "N": Nn, "K": K, "lib": os.path.basename(a.lib) or "libcp25.so"}
         res = {"lib": [], "own": []}
         if a.fp8:
             q, s = N.quant_fp8_rows(x)
@@ -65,6 +73,9 @@ def main():
             res["own"].append(timed(lambda: N.gemm_epi(x, w, out=out)))
         rec.update(kind="bf16", hipblaslt_ms=res["lib"], own_ms=res["own"],
                    hipblaslt_tflops=flop / min(res["lib"]) / 1e9, own_tflops=flop / min(res["own"]) / 1e9)
+        if a.plain:
+            print(json.dumps(rec), flush=True)
+            continue
         if name == "mlp1":
             def unfused():
                 torch.matmul(x, w.t(), out=out)
