@@ -305,9 +305,10 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }  // 256 B of zeros (static storage)
 
-template <int NT, int TW>
-__global__ void __launch_bounds__(256, 1) conv3x3_halo_kernel(ConvArgs a) {
+template <int NT, int TW, int NW>
+__global__ void __launch_bounds__(64 * NW, 1) conv3x3_halo_kernel(ConvArgs a) {
   constexpr int BN = 32 * NT;
+  constexpr int FPW = 16 / NW;                     // 32-pixel fragments per wave (16 per 512-pixel tile)
   constexpr int TH = 512 / TW;
   constexpr int HWD = TW + 2, HHT = TH + 2;
   constexpr int NHP = HWD * HHT;                   // halo pixels
@@ -318,10 +319,11 @@ __global__ void __launch_bounds__(256, 1) conv3x3_halo_kernel(ConvArgs a) {
   constexpr int HALO_BYTES = HALO_INS * 1024;
   constexpr int STAGE = HALO_BYTES + W_INS * 1024;
   constexpr int N_INS = HALO_INS + W_INS;
-  constexpr int INS_PER_WAVE = N_INS / 4;
+  constexpr int INS_PER_WAVE = (N_INS + NW - 1) / NW;  // the most any wave issues per stage (waves >= N_INS % NW
+                                                       // issue one fewer when NW does not divide N_INS)
   constexpr int FPR = TW / 32;                     // fragments per tile row
   constexpr int NBUF = 3;                          // LDS ring: stage s + 2's DMA in flight while s is multiplied
-  static_assert(N_INS % 4 == 0 && NBUF * STAGE <= 160 * 1024, "halo conv LDS");
+  static_assert(N_INS % 4 == 0 && NBUF * STAGE <= 160 * 1024 && (NW == 4 || NW == 8), "halo conv LDS");
   __shared__ __attribute__((aligned(16))) char smem[NBUF * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -337,7 +339,7 @@ __global__ void __launch_bounds__(256, 1) conv3x3_halo_kernel(ConvArgs a) {
   const int kc = a.Cin / 16;
   const int nst = a.KT * kc;
 
-  // ---- this lane's DMA sources (stage independent part): instruction i = wave + 4 u
+  // ---- this lane's DMA sources (stage independent part): instruction i = wave + NW u
   //   halo: pixel offset (hi * Win + wi) * Cin + 8 half, or -1 (zero page)
   //   weights: ((cout * KT) * 9 + tap) * Cin + 8 half, or -1; + kt * 9 * Cin + c16 * 16 per stage
   // lane l of a DMA instruction moves 16 B (8 channels) of pixel / cout l % 32, channel half l / 32: the LDS images
@@ -347,7 +349,7 @@ __global__ void __launch_bounds__(256, 1) conv3x3_halo_kernel(ConvArgs a) {
   int src_off[INS_PER_WAVE];
 #pragma unroll
   for (int u = 0; u < INS_PER_WAVE; ++u) {
-    const int i = wave + 4 * u;
+    const int i = wave + NW * u;  // (i >= N_INS: this wave has one instruction fewer; never issued)
     int off = -1;  // -1: the zero page
     if (i < HALO_INS) {
       const int h = i * 32 + sub;
@@ -386,7 +388,8 @@ __global__ void __launch_bounds__(256, 1) conv3x3_halo_kernel(ConvArgs a) {
     char* base = smem + buf * STAGE;
 #pragma unroll
     for (int u = 0; u < INS_PER_WAVE; ++u) {
-      const int i = wave + 4 * u;
+      const int i = wave + NW * u;
+      if (N_INS % NW != 0 && i >= N_INS) break;  // wave-uniform
       {
         const unsigned short* src;
         char* dst;
@@ -402,24 +405,40 @@ __global__ void __launch_bounds__(256, 1) conv3x3_halo_kernel(ConvArgs a) {
     }
   };
 
-  f32x16 acc[4][NT];
+  // counted wait for the stage after next: this wave's DMA instructions of one stage stay in flight
+  const bool short_wave = N_INS % NW != 0 && wave >= N_INS % NW;
+  auto wait_stage_dma = [&](auto LGK) __attribute__((always_inline)) {
+    if (short_wave) {
+      if constexpr (decltype(LGK)::value)
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(INS_PER_WAVE - 1) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(INS_PER_WAVE - 1) : "memory");
+    } else {
+      if constexpr (decltype(LGK)::value)
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(INS_PER_WAVE) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(INS_PER_WAVE) : "memory");
+    }
+  };
+
+  f32x16 acc[FPW][NT];
 #pragma unroll
-  for (int f = 0; f < 4; ++f)
+  for (int f = 0; f < FPW; ++f)
 #pragma unroll
     for (int j = 0; j < NT; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[f][j][r] = 0.f;
 
-  // fragment f of this wave: tile row (4 wave + f) / FPR, columns ((4 wave + f) % FPR) 32 + [0, 32); its halo
+  // fragment f of this wave: tile row (FPW wave + f) / FPR, columns ((FPW wave + f) % FPR) 32 + [0, 32); its halo
   // pixel for tap (kh, kw) is h = h0[f] + kh HWD + kw, at byte (h / 32) 1024 + hl 512 + (h % 32) 16
-  int h0[4];
+  int h0[FPW];
 #pragma unroll
-  for (int f = 0; f < 4; ++f) {
-    const int q = wave * 4 + f;
+  for (int f = 0; f < FPW; ++f) {
+    const int q = wave * FPW + f;
     h0[f] = (q / FPR) * HWD + (q % FPR) * 32 + l31;
   }
   const int b_base = HALO_BYTES + hl * 512 + l31 * 16;
-  static_assert(NT == 3, "the counted LDS waits below assume 3 + 4 fragment reads per tap");
+  static_assert(NT == 3, "the counted LDS waits below assume 3 + FPW fragment reads per tap");
   typedef __attribute__((address_space(3))) const char* lds_cptr;
   const unsigned smem_lds = (unsigned)(uintptr_t)(lds_cptr)smem;
 
@@ -429,7 +448,7 @@ __global__ void __launch_bounds__(256, 1) conv3x3_halo_kernel(ConvArgs a) {
   issue(0, 0);
   if (nst > 1) {
     issue(1, 1);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(INS_PER_WAVE) : "memory");
+    wait_stage_dma(std::false_type{});
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -438,19 +457,19 @@ __global__ void __launch_bounds__(256, 1) conv3x3_halo_kernel(ConvArgs a) {
   int buf = 0;
   for (int st = 0; st < nst; ++st) {
     if (st + 2 < nst) issue(st + 2, buf == 0 ? 2 : buf - 1);
-    // fragments of tap t + 1 are read (inline asm, 3 B + 4 A reads) while tap t's 12 MFMAs issue, behind a
-    // counted lgkmcnt(7) tied to tap t's registers (the compiler's own waits here were lgkmcnt(0): a full LDS
+    // fragments of tap t + 1 are read (inline asm, 3 B + FPW A reads) while tap t's 3 FPW MFMAs issue, behind a
+    // counted lgkmcnt(3 + FPW) tied to tap t's registers (the compiler's own waits here were lgkmcnt(0): a full LDS
     // latency every other tap)
     const unsigned sbase = smem_lds + buf * STAGE;
     const unsigned b_addr = sbase + b_base;
-    bf16x8 xa[2][4], wb[2][NT];
-    auto load_tap = [&](auto TC, bf16x8(&xs)[4], bf16x8(&ws)[NT]) __attribute__((always_inline)) {
+    bf16x8 xa[2][FPW], wb[2][NT];
+    auto load_tap = [&](auto TC, bf16x8(&xs)[FPW], bf16x8(&ws)[NT]) __attribute__((always_inline)) {
       constexpr int tap = decltype(TC)::value, kh = tap / 3, kw = tap % 3;
 #pragma unroll
       for (int j = 0; j < NT; ++j)
         asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ws[j]) : "v"(b_addr), "i"((tap * NT + j) * 1024));
 #pragma unroll
-      for (int f = 0; f < 4; ++f) {
+      for (int f = 0; f < FPW; ++f) {
         const int h = h0[f] + kh * HWD + kw;
         const unsigned ad = sbase + (h >> 5) * 1024 + hl * 512 + (h & 31) * 16;
         asm volatile("ds_read_b128 %0, %1" : "=v"(xs[f]) : "v"(ad));
@@ -461,24 +480,25 @@ __global__ void __launch_bounds__(256, 1) conv3x3_halo_kernel(ConvArgs a) {
       constexpr int tap = decltype(TC)::value, cur = tap & 1;
       if constexpr (tap + 1 < 9) {
         load_tap(std::integral_constant<int, tap + 1>{}, xa[cur ^ 1], wb[cur ^ 1]);
-        asm volatile("s_waitcnt lgkmcnt(7)"
-                     : "+v"(wb[cur][0]), "+v"(wb[cur][1]), "+v"(wb[cur][2]), "+v"(xa[cur][0]), "+v"(xa[cur][1]),
-                       "+v"(xa[cur][2]), "+v"(xa[cur][3]));
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(NT + FPW));
       } else {
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(wb[cur][0]), "+v"(wb[cur][1]), "+v"(wb[cur][2]), "+v"(xa[cur][0]), "+v"(xa[cur][1]),
-                       "+v"(xa[cur][2]), "+v"(xa[cur][3]));
+        asm volatile("s_waitcnt lgkmcnt(0)");
       }
+      // tap t's operands are ready only after the wait: pin them behind it
+#pragma unroll
+      for (int j = 0; j < NT; ++j) asm volatile("" : "+v"(wb[cur][j]));
+#pragma unroll
+      for (int f = 0; f < FPW; ++f) asm volatile("" : "+v"(xa[cur][f]));
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int f = 0; f < 4; ++f)
+      for (int f = 0; f < FPW; ++f)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
           acc[f][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb[cur][j], xa[cur][f], acc[f][j], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     });
     if (st + 2 < nst)
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(INS_PER_WAVE) : "memory");
+      wait_stage_dma(std::true_type{});
     else
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -491,8 +511,8 @@ __global__ void __launch_bounds__(256, 1) conv3x3_halo_kernel(ConvArgs a) {
   constexpr int OST = BN * 2 + 8;
   static_assert(512 * OST <= NBUF * STAGE, "halo conv epilogue staging");
 #pragma unroll
-  for (int f = 0; f < 4; ++f) {
-    const int px = (wave * 4 + f) * 32 + l31;  // tile pixel (fragment-major = row-major within the tile)
+  for (int f = 0; f < FPW; ++f) {
+    const int px = (wave * FPW + f) * 32 + l31;  // tile pixel (fragment-major = row-major within the tile)
 #pragma unroll
     for (int j = 0; j < NT; ++j)
 #pragma unroll
@@ -512,7 +532,7 @@ __global__ void __launch_bounds__(256, 1) conv3x3_halo_kernel(ConvArgs a) {
   const int M = a.Ho * a.Wo;
   constexpr int CPP = BN / 8;  // 16-B chunks per pixel
   const bool vec_ok = (a.Cout % 8) == 0 && n0 + BN <= a.Cout;
-  for (int idx = tid; idx < 512 * CPP; idx += 256) {
+  for (int idx = tid; idx < 512 * CPP; idx += 64 * NW) {
     const int px = idx / CPP, c = idx % CPP;
     const int q = px >> 5;
     const int ho = th0 + q / FPR, wo = tw0 + (q % FPR) * 32 + (px & 31);
@@ -538,11 +558,11 @@ __global__ void __launch_bounds__(256, 1) conv3x3_halo_kernel(ConvArgs a) {
   }
 }
 
-template <int NT, int TW>
+template <int NT, int TW, int NW = 4>
 int launch_conv_halo(const ConvArgs& a, hipStream_t s) {
   constexpr int TH = 512 / TW;
   dim3 grid((unsigned)(cdiv(a.Ho, TH) * (a.Wo / TW) * a.Tout), (unsigned)cdiv(a.Cout, 32 * NT), 1u);
-  hipLaunchKernelGGL((conv3x3_halo_kernel<NT, TW>), grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL((conv3x3_halo_kernel<NT, TW, NW>), grid, dim3(64 * NW), 0, s, a);
   CP25_LAUNCH_CHECK();
   return CP25_OK;
 }
@@ -633,10 +653,15 @@ extern "C" int cp25_conv3d(const void* const* frames, int n_frames, const void* 
   const bool halo_ok = KH == 3 && KW == 3 && stride_hw == 1 && out_split == 0 && pad_left == 1 && pad_right == 1 &&
                        Cout >= 64 && KT <= 3 && a.Wo % 32 == 0 &&
                        (int64_t)Hin * Win * Cin < (1LL << 31) && (int64_t)Cout * KT * 9 * Cin < (1LL << 31) &&
-                       g_conv_select == 0;
+                       g_conv_select != 1;
   if (halo_ok) {
     const int tw = a.Wo % 128 == 0 ? 128 : (a.Wo % 64 == 0 ? 64 : 32);
     // BN = 96 for every Cout (96 / 192 / 384 in the decoder): with BN = 128 the 256 accumulators spill
+    if (g_conv_select == 2) {  // 8 waves (two per SIMD), 2 fragments each
+      if (tw == 128) return launch_conv_halo<3, 128, 8>(a, stream);
+      if (tw == 64) return launch_conv_halo<3, 64, 8>(a, stream);
+      return launch_conv_halo<3, 32, 8>(a, stream);
+    }
     if (tw == 128) return launch_conv_halo<3, 128>(a, stream);
     if (tw == 64) return launch_conv_halo<3, 64>(a, stream);
     return launch_conv_halo<3, 32>(a, stream);
@@ -656,7 +681,7 @@ extern "C" int cp25_conv3d(const void* const* frames, int n_frames, const void* 
 }
 
 extern "C" int cp25_conv3d_select(int mode) {
-  if (mode < 0 || mode > 1) return CP25_ERR_INVAL;
+  if (mode < 0 || mode > 2) return CP25_ERR_INVAL;
   const int prev = g_conv_select;
   g_conv_select = mode;
   return prev;

@@ -1,6 +1,7 @@
 """cp25_conv3d at the decoder's dominant shapes (704x1280 / 352x640 / 176x320, 3x3x3, 4 output frames): the halo
 kernel (default) vs the per-tap kernel (cp25_conv3d_select(1)), HIP events, interleaved rounds in one process.
-One JSON line per shape: ms and TFLOP/s (2 * 27 * Cin * Cout per output pixel)."""
+One JSON line per shape: ms and TFLOP/s (2 * 27 * Cin * Cout per output pixel). CONV_KINDS=halo,tap,halo8 picks the
+kernels (halo8: the 8-wave halo kernel, cp25_conv3d_select(2)); CONV_SHAPE=i one shape; ROUNDS=n."""
 import json
 import os
 import sys
@@ -39,15 +40,19 @@ for i, (cin, cout, H, W) in enumerate(SHAPES):
     b = torch.zeros(cout, device=dev, dtype=torch.bfloat16)
     conv = _Conv(w, b, dev)
     run = lambda: conv(frames, 4, H, W, pad=(1, 1, 1, 1))  # noqa: E731
-    res = {"halo": [], "tap": []}
+    modes = {"halo": 0, "tap": 1, "halo8": 2}
+    kinds = os.environ.get("CONV_KINDS", "halo,tap").split(",")
+    res = {k: [] for k in kinds}
     for _ in range(int(os.environ.get("ROUNDS", "2"))):
-        for k in ("halo", "tap"):
-            prev = N.conv3d_select(1 if k == "tap" else 0)
+        for k in kinds:
+            prev = N.conv3d_select(modes[k])
             res[k].append(timed(run))
             N.conv3d_select(prev)
     flop = 2.0 * 27 * cin * cout * H * W * 4
-    rec = {"conv": f"{cin}->{cout} 3x3x3 {H}x{W} x4 frames", "halo_ms": min(res["halo"]), "tap_ms": min(res["tap"]),
-           "halo_tflops": flop / min(res["halo"]) / 1e9, "tap_tflops": flop / min(res["tap"]) / 1e9}
+    rec = {"conv": f"{cin}->{cout} 3x3x3 {H}x{W} x4 frames"}
+    for k in kinds:
+        rec[f"{k}_ms"] = min(res[k])
+        rec[f"{k}_tflops"] = flop / min(res[k]) / 1e9
     print(json.dumps(rec), flush=True)
 
 # VAE AttentionBlock core at 704 x 1280 (88 x 160 = 14 080 tokens, one frame): cp25_vae_attn vs the round-1
