@@ -280,7 +280,8 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
 // ---------------------------------------------------------------- 3x3 stride-1 conv with an LDS halo tile
 // The 3x3(x3) convs of the ResidualBlocks and the upsample Resample convs (pad 1 left / right; any top / bottom
 // pad, so the row bands of the banded decode take the same kernel and the same summation order). A workgroup
-// (4 waves, one per SIMD) owns a TH x TW output tile (512 pixels: each wave 4 fragments of 32 pixels of a row)
+// (NW = 8 waves, two per SIMD, so one wave's LDS / DMA waits are covered by its partner's MFMAs; or NW = 4, one per
+// SIMD) owns a TH x TW output tile (512 pixels: each wave 16 / NW fragments of 32 pixels of a row)
 // x BN = 32 NT output channels, and walks the K dimension in stages of (temporal tap kt, 16 input channels):
 //   * per stage the (TH + 2) x (TW + 2) input halo (16 channels, 32 B per pixel) and the 9 x BN weight rows of
 //     the stage land in LDS by LDS-DMA (global_load_lds_dwordx4, 32 pixels / couts per wave instruction;
@@ -558,7 +559,7 @@ __global__ void __launch_bounds__(64 * NW, 1) conv3x3_halo_kernel(ConvArgs a) {
   }
 }
 
-template <int NT, int TW, int NW = 4>
+template <int NT, int TW, int NW>
 int launch_conv_halo(const ConvArgs& a, hipStream_t s) {
   constexpr int TH = 512 / TW;
   dim3 grid((unsigned)(cdiv(a.Ho, TH) * (a.Wo / TW) * a.Tout), (unsigned)cdiv(a.Cout, 32 * NT), 1u);
@@ -657,14 +658,16 @@ extern "C" int cp25_conv3d(const void* const* frames, int n_frames, const void* 
   if (halo_ok) {
     const int tw = a.Wo % 128 == 0 ? 128 : (a.Wo % 64 == 0 ? 64 : 32);
     // BN = 96 for every Cout (96 / 192 / 384 in the decoder): with BN = 128 the 256 accumulators spill
-    if (g_conv_select == 2) {  // 8 waves (two per SIMD), 2 fragments each
-      if (tw == 128) return launch_conv_halo<3, 128, 8>(a, stream);
-      if (tw == 64) return launch_conv_halo<3, 64, 8>(a, stream);
-      return launch_conv_halo<3, 32, 8>(a, stream);
+    // 8 waves (two per SIMD, 2 fragments each; the default): 8-16 % faster than 4 waves (one per SIMD, 4
+    // fragments each, cp25_conv3d_select(2)) at the decoder's shapes, bit-identical (profiles/r3/conv/)
+    if (g_conv_select == 2) {
+      if (tw == 128) return launch_conv_halo<3, 128, 4>(a, stream);
+      if (tw == 64) return launch_conv_halo<3, 64, 4>(a, stream);
+      return launch_conv_halo<3, 32, 4>(a, stream);
     }
-    if (tw == 128) return launch_conv_halo<3, 128>(a, stream);
-    if (tw == 64) return launch_conv_halo<3, 64>(a, stream);
-    return launch_conv_halo<3, 32>(a, stream);
+    if (tw == 128) return launch_conv_halo<3, 128, 8>(a, stream);
+    if (tw == 64) return launch_conv_halo<3, 64, 8>(a, stream);
+    return launch_conv_halo<3, 32, 8>(a, stream);
   }
   const int bk = (Cin % 64 == 0) ? 64 : (Cin % 32 == 0 ? 32 : 16);
   int nt;

@@ -277,9 +277,9 @@ int cp25_conv3d(const void* const* frames, int n_frames, const void* weight, con
                 hipStream_t stream);
 
 /* Kernel choice of cp25_conv3d for the 3x3 stride-1 convs: 0 (default) the LDS-halo kernel where it applies, 1 the
- * per-tap implicit GEMM everywhere (A/B runs and tests; same arithmetic up to summation order), 2 the halo kernel with
- * 8 waves per workgroup (two per SIMD; bit-identical to 0). Returns the previous mode. The initial mode is read once at
- * library load from CP25_CONV_KERNEL ("tap" = 1). */
+ * per-tap implicit GEMM everywhere (A/B runs and tests; same arithmetic up to summation order), 2 the round-2 halo
+ * kernel with 4 waves per workgroup (one per SIMD; bit-identical to 0, which runs 8). Returns the previous mode. The
+ * initial mode is read once at library load from CP25_CONV_KERNEL ("tap" = 1). */
 int cp25_conv3d_select(int mode);
 
 /* y = F.normalize(x, dim=C) * sqrt(C) * gamma [then SiLU] per pixel of n_pix channels-last pixels,

@@ -2,7 +2,7 @@
 (ActionConditionedInference.generate, the reference's action_conditioned.py:205-380 chunk loop) at the
 Bridge resolution 480x640 (action/configs/action_conditioned/data.py:78), 13-frame chunks (12 new
 frames each), 35 UniPC steps, CFG 7, synthetic random-init weights, random initial frame and actions.
-Reports frames/s of the whole long video; --linear-precision fp8 runs the DiT block GEMMs in fp8.
+Reports frames/s of the whole long video; --linear-precision fp8 runs the DiT block GEMMs in fp8; --block-gemm lib puts them on the library (A/B).
 One JSON line. (CP = 4 needs four GPUs; this is the single-GPU rate of the same loop.)"""
 import argparse
 import json
@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--chunk-size", type=int, default=12)
     ap.add_argument("--linear-precision", default="bf16", choices=("bf16", "fp8"))
     ap.add_argument("--attention-precision", default="bf16", choices=("bf16", "fp8qk", "fp8"))
+    ap.add_argument("--block-gemm", default="own", choices=("own", "lib"),
+                    help="block projections on the hand-written GEMMs (default) or the library (A/B)")
     a = ap.parse_args()
     h, w = (int(x) for x in a.resolution.split(","))
     dev = torch.device("cuda:0")
@@ -34,6 +36,7 @@ def main():
     n_chunks = -(-(a.frames - 1) // a.chunk_size)
     inf = ActionConditionedInference(device=dev, state_t=1 + a.chunk_size // 4, linear_precision=a.linear_precision,
                                      attention_precision=a.attention_precision)
+    inf.pipe.model.net.block_gemm = a.block_gemm
     adim = inf.pipe.model.net.cfg.action_dim
     rng = np.random.RandomState(0)
     img = rng.randint(0, 256, size=(h, w, 3), dtype=np.uint8)
@@ -48,7 +51,7 @@ def main():
     assert video.shape == (a.frames, h, w, 3), video.shape
     print(json.dumps({"workload": f"action-conditioned AR {a.frames}f at {h}x{w}, {n_chunks} chunks of "
                                   f"{a.chunk_size + 1} frames, {a.num_steps} UniPC steps, CFG 7",
-                      "linear_precision": a.linear_precision,
+                      "linear_precision": a.linear_precision, "block_gemm": a.block_gemm,
                       "attention_precision": a.attention_precision, "n_gpus": 1, "seconds": dt,
                       "frames_per_s": a.frames / dt, "s_per_chunk": dt / n_chunks}), flush=True)
 

@@ -1,7 +1,7 @@
 """cp25_conv3d at the decoder's dominant shapes (704x1280 / 352x640 / 176x320, 3x3x3, 4 output frames): the halo
 kernel (default) vs the per-tap kernel (cp25_conv3d_select(1)), HIP events, interleaved rounds in one process.
-One JSON line per shape: ms and TFLOP/s (2 * 27 * Cin * Cout per output pixel). CONV_KINDS=halo,tap,halo8 picks the
-kernels (halo8: the 8-wave halo kernel, cp25_conv3d_select(2)); CONV_SHAPE=i one shape; ROUNDS=n."""
+One JSON line per shape: ms and TFLOP/s (2 * 27 * Cin * Cout per output pixel). CONV_KINDS=halo,tap,halo4 picks the
+kernels (halo: the 8-wave halo kernel, the default; halo4: the round-2 4-wave form, cp25_conv3d_select(2)); CONV_SHAPE=i one shape; ROUNDS=n."""
 import json
 import os
 import sys
@@ -40,7 +40,7 @@ for i, (cin, cout, H, W) in enumerate(SHAPES):
     b = torch.zeros(cout, device=dev, dtype=torch.bfloat16)
     conv = _Conv(w, b, dev)
     run = lambda: conv(frames, 4, H, W, pad=(1, 1, 1, 1))  # noqa: E731
-    modes = {"halo": 0, "tap": 1, "halo8": 2}
+    modes = {"halo": 0, "tap": 1, "halo4": 2}
     kinds = os.environ.get("CONV_KINDS", "halo,tap").split(",")
     res = {k: [] for k in kinds}
     for _ in range(int(os.environ.get("ROUNDS", "2"))):
