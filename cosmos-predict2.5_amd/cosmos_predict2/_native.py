@@ -87,6 +87,7 @@ SIGNATURES = {
                     _I, _I, _I, _I, _I, _I, _P],
     "cp25_rms_norm_silu": [_P, _P, _P, _I64, _I, _I, _P],
     "cp25_conv3d_select": [_I],
+    "cp25_attn_cross_select": [_I],
     "cp25_softmax_rows": [_P, _I64, _I, _I64, _F, _P, _I64, _P],
     "cp25_vae_attn": [_P, _I64, _I64, _P, _I64, _I64, _P, _I64, _I64, _P, _I64, _I64, _I, _I, _I, _I, _F, _P, _I64,
                       _P],
@@ -253,6 +254,14 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
     )
     _check("cp25_attn_fwd_bounded", rc)
     return out
+
+
+def attn_cross_select(form: int) -> int:
+    """cp25_attn_cross_select: the kernel form of short-key (text cross-attention) launches, 1 = persistent (default),
+    0 = one workgroup per query block (A/B and tests; bit-identical). Returns the previous form."""
+    rc = load_library().cp25_attn_cross_select(int(form))
+    _check("cp25_attn_cross_select", min(rc, 0))
+    return rc
 
 
 def attn_kernel_name(Lk: int, softmax_scale: Optional[float] = None, norm_bounds=None, prescaled: bool = False,

@@ -126,6 +126,13 @@ size_t cp25_attn_workspace_bytes(int B, int H, int Lq, int n_split);
  * one workgroup per CU), or a negative error code. */
 int cp25_attn_plan(int B, int H, int Lq, int Lk, int D);
 
+/* Kernel form of the short-key (Lk <= 4096: the text cross-attention, minimal_v4_dit.py:1216-1226) launches of
+ * cp25_attn_fwd / _bounded / _prescaled: 1 (default) the persistent form (one workgroup per CU walking a run of
+ * query blocks as one K/V tile stream, the next block's Q staged through LDS; unsplit launches in the zero-shift or
+ * online modes with Lk > 64), 0 one workgroup per query block. Both forms are bit-identical. Returns the previous
+ * form, or CP25_ERR_INVAL for another value. */
+int cp25_attn_cross_select(int form);
+
 /* ---------------------------------------------------------------- DiT block elementwise
  * Activations are token-major [n_tok, B, D] bf16 (batch inner). Row (tok, b) uses modulation row
  * (b, t) with t = (tok0 + tok) / hw (frame index; tok0 = first global token of this CP shard).

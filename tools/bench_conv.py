@@ -1,7 +1,8 @@
 """cp25_conv3d at the decoder's dominant shapes (704x1280 / 352x640 / 176x320, 3x3x3, 4 output frames): the halo
 kernel (default) vs the per-tap kernel (cp25_conv3d_select(1)), HIP events, interleaved rounds in one process.
 One JSON line per shape: ms and TFLOP/s (2 * 27 * Cin * Cout per output pixel). CONV_KINDS=halo,tap,halo4 picks the
-kernels (halo: the 8-wave halo kernel, the default; halo4: the round-2 4-wave form, cp25_conv3d_select(2)); CONV_SHAPE=i one shape; ROUNDS=n."""
+kernels (halo: the 8-wave halo kernel, the default; halo4: the round-2 4-wave form, cp25_conv3d_select(2)); CONV_SHAPE=i one shape; ROUNDS=n;
+CONV_LIB=path a lab build of libcp25.so (tools/lab/conv_variant.py) instead of the in-tree one."""
 import json
 import os
 import sys
@@ -13,6 +14,9 @@ import torch  # noqa: E402
 
 from cosmos_predict2 import _native as N  # noqa: E402
 from cosmos_predict2.vae import _Conv  # noqa: E402
+
+if os.environ.get("CONV_LIB"):
+    N._LIB_PATH = os.environ["CONV_LIB"]
 
 dev = torch.device("cuda:0")
 SHAPES = [(96, 96, 704, 1280), (192, 192, 352, 640), (384, 384, 176, 320), (384, 384, 88, 160)]

@@ -1,0 +1,107 @@
+#!/usr/bin/env python3
+"""Static checks of the gfx950 ISA of a HIP source (hipcc --cuda-device-only -S): per kernel, VGPRs / spills (the
+compiler's resource remarks), in-loop scratch and vmcnt(0), s_nop count, and LDS-read races: an instruction that reads
+or writes a VGPR while an LDS read into it is still in flight (not yet retired by an s_waitcnt lgkmcnt, counted in
+issue order). The hand-scheduled kernels issue ds_reads from inline asm whose destinations the compiler does not know
+are written asynchronously; if such an asm output is dead (e.g. its MFMA was eliminated) the register allocator may
+hand the register to another value while the read is in flight -- a silent wrong result this check catches.
+usage: python tools/isa_check.py file.hip [name-filter]   (exit 1 on any race)"""
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def compile_asm(src, out="/tmp/isa_check.s", extra=()):
+    unit_flags = ["-fno-honor-nans", "-fno-slp-vectorize"] if os.path.basename(src).startswith(("attn_fwd", "vae_attn")) \
+        else []  # the Makefile's per-unit flags
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+           "-fhip-fp32-correctly-rounded-divide-sqrt", "-I" + os.path.join(ROOT, "include"),
+           "-I" + os.path.join(ROOT, "cosmos-predict2.5_amd", "csrc"), *unit_flags,
+           "--cuda-device-only", "-S", src, "-o", out, "-Rpass-analysis=kernel-resource-usage", *extra]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode:
+        raise RuntimeError(r.stderr[-3000:])
+    res, cur = {}, None
+    for line in r.stderr.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            cur = m.group(1)
+            res[cur] = {}
+            continue
+        m = re.search(r"(VGPRs|VGPRs Spill|SGPRs Spill|LDS Size \[bytes/block\]): (\d+)", line)
+        if m and cur:
+            res[cur][m.group(1).split(" [")[0]] = int(m.group(2))
+    return open(out).read(), res
+
+
+def _regs(op):
+    m = re.match(r"v\[(\d+):(\d+)\]", op)
+    if m:
+        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    m = re.match(r"v(\d+)$", op)
+    return {int(m.group(1))} if m else set()
+
+
+def analyse(asm, name):
+    i = asm.index(name + ":")
+    j = asm.index(".Lfunc_end", i)
+    lines = asm[i:j].split("\n")
+    pending, races, nops = [], [], 0
+    inloop, scr, vm0 = False, 0, 0
+    for l in lines:
+        s = l.strip()
+        if not s or s.startswith(";"):
+            continue
+        if re.match(r"^\.LBB", l):
+            inloop = "Loop" in l
+            continue
+        t = s.replace(",", " ").split()
+        op = t[0]
+        if inloop and op.startswith("scratch_"):
+            scr += 1
+        if inloop and op == "s_waitcnt" and "vmcnt(0)" in s:
+            vm0 += 1
+        if op == "s_nop":
+            nops += 1
+        if op.startswith("ds_read"):
+            pending.append(_regs(t[1]))
+        elif op.startswith(("ds_", "s_load", "s_buffer_load")):
+            pending.append(set())
+        elif op == "s_waitcnt":
+            m = re.search(r"lgkmcnt\((\d+)\)", s)
+            if m:
+                n = int(m.group(1))
+                while len(pending) > n:
+                    pending.pop(0)
+        else:
+            live = set().union(*pending) if pending else set()
+            used = set()
+            for x in t[1:]:
+                used |= _regs(x)
+            if used & live:
+                races.append(s)
+    return {"races": races, "nops": nops, "inloop_scratch": scr, "inloop_vmcnt0": vm0}
+
+
+def check(src, flt=""):
+    asm, res = compile_asm(src)
+    out = {}
+    for name in re.findall(r"^(_Z\S+):", asm, re.M):
+        if flt in name:
+            out[name] = dict(res.get(name, {}), **analyse(asm, name))
+    return out
+
+
+if __name__ == "__main__":
+    rep = check(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "")
+    bad = 0
+    for name, r in rep.items():
+        bad += len(r["races"])
+        print(f"{name[:72]:72s} vgpr {r.get('VGPRs')} spill {r.get('VGPRs Spill')} | in-loop scratch "
+              f"{r['inloop_scratch']} vmcnt(0) {r['inloop_vmcnt0']} | s_nop {r['nops']} | LDS races {len(r['races'])}")
+        for s in r["races"][:3]:
+            print("    race:", s[:100])
+    sys.exit(1 if bad else 0)

@@ -139,22 +139,15 @@ constexpr int kLds16 = 2 * kKBuf16 + 2 * kVBuf16;  // 73728
 // the K/V pipeline never drains between blocks and a block's prologue (its Q) and epilogue (its O stores) hide
 // under the neighbouring tiles' work:
 //   * each wave copies its next block's Q fragments (8 KiB, in its own ds_read_b128 lane order) into a private LDS
-//     slot by LDS-DMA in the softmax phase of one of the block's tiles 0 .. ntk - 2 (kQCopyStagger), and reads them into its Q
-//     registers in the softmax phase of the block's last tile (after the last Q K^T of the old block, before the
-//     first of the new);
+//     slot by LDS-DMA, one 1-KiB piece at a time spread over the softmax phases of the block's tiles 0 .. ntk - 2
+//     (a whole 8-KiB copy in one phase stalled the next phase's staging wait on its HBM latency: -10 % when
+//     removed, profiles/r3/xattn_persistent/boundary_probe.log), and reads them into its Q registers in the softmax
+//     phase of the block's last tile (after the last Q K^T of the old block, before the first of the new);
 //   * the softmax phase that opens a block first normalises the finished block's O into the same slot as row-major
 //     bf16 rows and stores them from there as whole 256-B rows (four rows per store instruction instead of 16-B
-//     pieces of 16 rows at the token stride), then zeroes O. Isolation probes (lab builds without the copy / without the
-//     stores, profiles/r3/xattn_persistent/boundary_probe_v*.log): the copy's exposed HBM latency and the stores are
-//     what remains of the block seam.
+//     pieces of 16 rows at the token stride: the per-lane form cost -12 % when removed, same probe), then zeroes O.
 // Each block's arithmetic is the per-block kernel's, operation for operation (the online shift restarts from 0),
 // so the two forms are bit-identical. Needs ntk >= 2 (the last Q piece lands at least one phase pair before its read).
-// The next block's Q copy is issued whole (8 KiB per wave) in one softmax phase, at a tile that differs between
-// workgroups (kQCopyStagger). Issued at tile 0 in every workgroup it was a chip-wide burst of 256 x 64 KiB at once whose
-// HBM latency the staging wait two phases later (in-order vmcnt) waited out: -10 % without the copy
-// (boundary_probe_v1.log). Spread one piece per tile it measured slower still (every tile then waits on a piece,
-// boundary_probe_v2.log).
-constexpr bool kQCopyStagger = true;
 constexpr int kOStr = 272;                          // staged O row stride (256 B + 16: conflict-free b64 writes)
 constexpr int kQSlot = kQRows * kOStr;              // per wave 8704 B: next-block Q fragments (8 KiB) / staged O rows
 constexpr int kLdsP = kLds16 + kWaves * kQSlot;     // 143360
@@ -241,7 +234,6 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
   for (int qh = 0; qh < 2; ++qh) minit[qh] = f32x4{-m_run[qh], -m_run[qh], -m_run[qh], -m_run[qh]};
 
   const int ntiles = kPersist ? (blk_end - blk0) * ntk : ntk;
-  const int copy_tile = kPersist && ntk > 1 ? (kQCopyStagger ? (int)(blockIdx.x % (unsigned)(ntk - 1)) : 0) : 0;
 
   // staging: a group's 256 threads own rows u/16 + 16 i, chunk u%16 of a 64 x 128 tile. buffer_load with a
   // wave-uniform descriptor (SALU-only addressing); rows past Lk fall outside its range and read as zero (their
@@ -413,9 +405,12 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
       tb = t_run / ntk;
       t = t_run - tb * ntk;
       if (t == 0 && tb > 0) store_block(blk0 + tb - 1);
-      // the next block's Q copy, whole, in the softmax phase of tile (workgroup mod (ntk - 1)): the workgroups' block
-      // seams run in lock step, so a copy at tile 0 everywhere was one chip-wide HBM burst per block
-      if (t == copy_tile && blk0 + tb + 1 < blk_end) dma_q(blk0 + tb + 1, 0, 8);
+      // the next block's Q copy: piece p in the softmax phase of tile p (ntk - 1) / 8 (tiles 0 .. ntk - 2)
+      const int n_iss = ntk - 1;
+      if (t < n_iss && blk0 + tb + 1 < blk_end) {
+        const int p_lo = (8 * t + n_iss - 1) / n_iss, p_hi = min((8 * (t + 1) + n_iss - 1) / n_iss, 8);
+        if (p_lo < p_hi) dma_q(blk0 + tb + 1, p_lo, p_hi);
+      }
     }
     if (__builtin_expect(t == ragged_tile, 0)) {
 #pragma unroll
@@ -565,13 +560,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
         for (int i = 1; i <= kAhead; ++i) p += nreads(n + i);
         return p;
       }();
-      // The wait READS the operand ("v" input) and a scheduling barrier keeps the MFMAs behind it. An input keeps the
-      // asynchronously written register allocated until its data has landed (also when the MFMAs that use it are
-      // dead, as in the Q K^T after the last tile); the previous form, an asm "redefining" it ("+v"), made the hazard
-      // recognizer treat it as a VALU write and pad every MFMA pair with an s_nop (-2.3 % per launch without them,
-      // profiles/r3/attn_nop/self_nop_ab.log).
-      asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(pending), "v"(ring[n % kR]) : "memory");
-      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(ring[n % kR]) : "i"(pending));
 #pragma unroll
       for (int qh = 0; qh < 2; ++qh) {
         if constexpr (n >= 16) {

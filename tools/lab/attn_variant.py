@@ -1,0 +1,48 @@
+"""Lab builds of libcp25.so with a text-patched attn_fwd.hip (isolation variants of the persistent cross-attention's
+block boundary, for same-box A/B with tools/bench_xattn.py --lib; results are WRONG for every patch except 'none').
+The product source is not touched: the patched copy is compiled from /tmp and linked with the in-tree objects.
+usage: python tools/lab/attn_variant.py <name> <patch>[,<patch>...]  ->  tools/lab/libcp25_<name>.so
+patches: nostore (no O stores at block boundaries), nodma (no next-block Q copy), noqread (no Q read from LDS),
+nostagger (the Q copy at tile 0 in every workgroup; correct results), none"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+CSRC = os.path.join(ROOT, "cosmos-predict2.5_amd", "csrc")
+OBJ = os.path.join(ROOT, "cosmos-predict2.5_amd", "cosmos_predict2", "_lib", "obj")
+
+PATCHES = {
+    "nostore": [("      if (row0 + r < a.Lq) *reinterpret_cast<u32x4*>(wo + (int64_t)(row0 + r) * a.o_sl) = v;\n",
+                 "      if (row0 + r < 0) *reinterpret_cast<u32x4*>(wo + (int64_t)(row0 + r) * a.o_sl) = v;\n")],
+    "nodma": [("      if (t == copy_tile && blk0 + tb + 1 < blk_end) dma_q(blk0 + tb + 1, 0, 8);\n",
+               "      if (t == copy_tile && blk0 + tb + 1 < 0) dma_q(blk0 + tb + 1, 0, 8);\n")],
+    "noqread": [("      if (t == ntk - 1 && blk0 + tb + 1 < blk_end) {\n",
+                 "      if (t == ntk - 1 && blk0 + tb + 1 < 0) {\n")],
+    "nostagger": [("constexpr bool kQCopyStagger = true;\n", "constexpr bool kQCopyStagger = false;\n")],  # correct
+    "none": [],
+}
+
+
+def main():
+    name, patches = sys.argv[1], sys.argv[2].split(",")
+    src = open(os.path.join(CSRC, "attn_fwd.hip")).read()
+    for p in patches:
+        for old, new in PATCHES[p]:
+            assert src.count(old) == 1, (p, old)
+            src = src.replace(old, new)
+    tmp = f"/tmp/attn_{name}.hip"
+    open(tmp, "w").write(src)
+    subprocess.check_call(["make", "-s", "-C", CSRC, "-j8"])
+    flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-fhip-fp32-correctly-rounded-divide-sqrt",
+             "-fno-honor-nans", "-fno-slp-vectorize", "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
+    subprocess.check_call(["/opt/rocm/bin/hipcc", *flags, "-c", tmp, "-o", f"/tmp/attn_{name}.o"])
+    others = [os.path.join(OBJ, f + ".o") for f in ("dit_ops", "fp8_ops", "gemm", "unipc", "vae_attn", "vae_ops")]
+    out = os.path.join(ROOT, "tools", "lab", f"libcp25_{name}.so")
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out,
+                           f"/tmp/attn_{name}.o", *others])
+    print(out)
+
+
+if __name__ == "__main__":
+    main()

@@ -485,13 +485,11 @@ __global__ void __launch_bounds__(64 * NW, 1) conv3x3_halo_kernel(ConvArgs a) {
       } else {
         asm volatile("s_waitcnt lgkmcnt(0)");
       }
-      // tap t's operands are ready only after the wait: the pins READ them there (keeping the asynchronously written
-      // registers allocated until the data has landed) and the scheduling barrier keeps the MFMAs behind them (an
-      // operand-redefining "+v" pin reads as a VALU write to the hazard recognizer: an s_nop before every tap's MFMAs)
+      // tap t's operands are ready only after the wait: pin them behind it
 #pragma unroll
-      for (int j = 0; j < NT; ++j) asm volatile("" ::"v"(wb[cur][j]));
+      for (int j = 0; j < NT; ++j) asm volatile("" : "+v"(wb[cur][j]));
 #pragma unroll
-      for (int f = 0; f < FPW; ++f) asm volatile("" ::"v"(xa[cur][f]));
+      for (int f = 0; f < FPW; ++f) asm volatile("" : "+v"(xa[cur][f]));
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int f = 0; f < FPW; ++f)
