@@ -54,6 +54,8 @@ SIGNATURES = {
                             _P, ctypes.c_size_t, _P],
     "cp25_attn_fwd_bounded": [_P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, c_int64_p, _F, _F,
                               _F, _I, _P, ctypes.c_size_t, _P],
+    "cp25_attn_fwd_prescaled_kslots": [_P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, c_int64_p,
+                                       _F, _F, _P, _I, _I, _P, ctypes.c_size_t, _P],
     "cp25_attn_fwd_prescaled": [_P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, c_int64_p, _F,
                                 _F, _I, _P, ctypes.c_size_t, _P],
     "cp25_attn_fwd_prescaled_fp8qk": [_P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, c_int64_p, _F,
@@ -71,6 +73,7 @@ SIGNATURES = {
     "cp25_final_ln_mod": [_P, _P, _P, _I64, _I64, _P, _P, _I64, _I64, _P, _I64, _I, _I, _I64, _I64, _F, _P],
     "cp25_head_rmsnorm_rope": [_P, _I64, _I64, _I, _I, _I, _P, _P, _P, _P, _I64, _F, _P],
     "cp25_head_rmsnorm_rope_scaled": [_P, _I64, _I64, _I, _I, _I, _P, _P, _P, _P, _I64, _F, _F, _P],
+    "cp25_head_rmsnorm_rope_nmax": [_P, _I64, _I64, _I, _I, _I, _P, _P, _P, _P, _I64, _F, _F, _P, _P],
     "cp25_copy_rows": [_P, _I64, _P, _I64, _I64, _I64, _P],
     "cp25_gelu": [_P, _I64, _P],
     "cp25_gemm_epi": [_P, _I64, _P, _I64, _P, _I64, _I, _I, _I, _I, _P],
@@ -179,7 +182,8 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
              softmax_scale: Optional[float] = None, n_split: Optional[int] = None,
              norm_bounds: Optional[Tuple[float, float]] = None, prescaled: bool = False,
              fp8_qk: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-             fp8_v: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+             fp8_v: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+             k_norm_slots: Optional[torch.Tensor] = None) -> torch.Tensor:
     """softmax(q k^T * scale) v for q [B, Lq, H, 128], k/v [B, Lk, H, 128] (bf16, any strides with
     a contiguous head dim). Returns [B, Lq, H, 128] bf16. n_split: key-range split (None = the
     library's plan for this shape; the fp32 partials live in a caching-allocator workspace).
@@ -191,7 +195,9 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
     cast_fp8(q * 2^s), cast_fp8(k * 2^-s); cp25_attn_fwd_prescaled_fp8qk; needs bounds with product <= 60); q / k
     are then only shape references. fp8_v=(v8t, v_amax) (with fp8_qk; from cast_v_fp8t(v)): P.V on e5m2 P and
     e4m3 V too (cp25_attn_fwd_prescaled_fp8; needs 1.13 x the bound product <= 30); v is then only a shape
-    reference."""
+    reference. k_norm_slots (with prescaled, bf16): the float32 [64, 32] slots head_rmsnorm_rope(norm_max=...) filled
+    for k, a data-tight key bound (cp25_attn_fwd_prescaled_kslots: blocks whose bound allows it run the zero-shift
+    loop even when norm_bounds do not)."""
     lib = load_library()
     if q.dtype != torch.bfloat16 or k.dtype != torch.bfloat16 or v.dtype != torch.bfloat16:
         raise ValueError("attn_fwd expects bf16 q/k/v (attention() recasts to bf16 first)")
@@ -240,6 +246,14 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
                                                    qb, kb, int(n_split), _ptr(ws), ws_bytes, _stream(q.device))
             _check("cp25_attn_fwd_prescaled_fp8qk", rc)
             return out
+        if k_norm_slots is not None:
+            if k_norm_slots.dtype != torch.float32 or k_norm_slots.numel() != 2048 or not k_norm_slots.is_contiguous():
+                raise ValueError("k_norm_slots: a contiguous float32 [64, 32] slot buffer expected")
+            rc = lib.cp25_attn_fwd_prescaled_kslots(_ptr(q), _ptr(k), _ptr(v), _ptr(out), B, H, Lq, Lk, D, *strides, qb,
+                                                    kb, _ptr(k_norm_slots), 64, int(n_split), _ptr(ws), ws_bytes,
+                                                    _stream(q.device))
+            _check("cp25_attn_fwd_prescaled_kslots", rc)
+            return out
         rc = lib.cp25_attn_fwd_prescaled(_ptr(q), _ptr(k), _ptr(v), _ptr(out), B, H, Lq, Lk, D, *strides, qb, kb,
                                          int(n_split), _ptr(ws), ws_bytes, _stream(q.device))
         _check("cp25_attn_fwd_prescaled", rc)
@@ -267,7 +281,7 @@ def attn_cross_select(form: int) -> int:
 def attn_kernel_name(Lk: int, softmax_scale: Optional[float] = None, norm_bounds=None, prescaled: bool = False,
                      fp8: int = 0) -> str:
     """The kernel form attn_fwd launches for these arguments (cp25_attn_kernel), e.g.
-    'attn_fwd_m16<self, prescaled, online max>'."""
+    'attn_fwd_m16<self, prescaled, online max>'; prescaled = 2: the k_norm_slots form."""
     qb, kb = (0.0, 0.0) if norm_bounds is None else (float(norm_bounds[0]), float(norm_bounds[1]))
     sc = 128 ** -0.5 if softmax_scale is None else float(softmax_scale)
     return load_library().cp25_attn_kernel(int(Lk), sc, qb, kb, int(prescaled), int(fp8)).decode()
@@ -379,11 +393,15 @@ def final_ln_mod(x: torch.Tensor, shift: torch.Tensor, scale: torch.Tensor, *, n
 def head_rmsnorm_rope(buf: torch.Tensor, *, n_rows: int, B: int, H: int, head_off: int, weight: torch.Tensor,
                       cos: Optional[torch.Tensor] = None, sin: Optional[torch.Tensor] = None,
                       out2: Optional[torch.Tensor] = None, out2_stride: int = 0, eps: float = 1e-6,
-                      out_scale: float = 1.0) -> None:
+                      out_scale: float = 1.0, norm_max: Optional[torch.Tensor] = None) -> None:
+    """norm_max: float32 [64, 32] slots (zeroed by the caller; slot i = norm_max[i, 0]) that receive the max |row| of the
+    result by atomic max (cp25_head_rmsnorm_rope_nmax): the data-tight key bound attn_fwd(k_norm_slots=...) reads."""
     lib = load_library()
-    rc = lib.cp25_head_rmsnorm_rope_scaled(
+    if norm_max is not None and (norm_max.dtype != torch.float32 or norm_max.numel() != 2048 or not norm_max.is_contiguous()):
+        raise ValueError("norm_max: a contiguous float32 [64, 32] slot buffer expected")
+    rc = lib.cp25_head_rmsnorm_rope_nmax(
         _ptr(buf), buf.stride(-2) if buf.dim() >= 2 else buf.shape[-1], n_rows, B, H, head_off, _ptr(weight),
-        _ptr(cos), _ptr(sin), _ptr(out2), out2_stride, eps, out_scale, _stream(buf.device),
+        _ptr(cos), _ptr(sin), _ptr(out2), out2_stride, eps, out_scale, _ptr(norm_max), _stream(buf.device),
     )
     _check("cp25_head_rmsnorm_rope", rc)
 

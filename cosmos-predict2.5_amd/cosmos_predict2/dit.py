@@ -217,6 +217,10 @@ class MinimalV1LVGDiT:
         # cross-output and MLP layer2 projections, so each LN-mod reads the new x once); "lib" = hipBLASLt GEMMs with
         # the GELU and the residuals in the elementwise kernels (the round-2 path, kept for A/B)
         self.block_gemm = "own"
+        # single-GPU self-attention with weight-based norm bounds past the zero-shift window (trained q/k norm weights):
+        # the k RMSNorm kernel measures max |k| (64 device slots) and the attention runs the gated pair, the
+        # zero-shift loop for every 256-query block whose data-tight bound allows it (cp25_attn_fwd_prescaled_kslots)
+        self.data_tight_k_bound = True
 
     def set_linear_precision(self, precision: str) -> None:
         """"bf16" (default, the reference's arithmetic) or "fp8": the 28 blocks' q/k/v, output, cross-q,
@@ -272,6 +276,17 @@ class MinimalV1LVGDiT:
         `exact_q_rounding = True` keeps the reference's rounding point (q rounded, scale applied to the fp32
         scores)."""
         return self._attn_mode(self.attn_bounds[i], hd)
+
+    def _k_slots(self, attn_kw: dict) -> Optional[torch.Tensor]:
+        """Zeroed max-|k| slots for a prescaled bf16 self-attention whose weight-based bounds exceed the zero-shift
+        window (data_tight_k_bound), else None. Single-GPU only: the gated pair picks a row's mode per 256-query
+        block, which context-parallel shards (bit-identical to CP = 1 by contract) must not depend on."""
+        if not (self.data_tight_k_bound and attn_kw.get("prescaled") and self.attention_precision == "bf16"):
+            return None
+        qb, kb = attn_kw["norm_bounds"]
+        if qb * kb <= 96.0:
+            return None
+        return torch.zeros((64, 32), dtype=torch.float32, device=self.device)
 
     def _attn_mode(self, bounds, hd: int):
         """The rule of _self_attn_mode for any RMS-normed q / k pair (also the text cross-attention)."""
@@ -414,7 +429,10 @@ class MinimalV1LVGDiT:
             if name == "self" and kw.get("prescaled") and self.attention_precision != "bf16":
                 qb, kb = kw["norm_bounds"]
                 fp8 = 0 if qb * kb > 60.0 else (2 if self.attention_precision == "fp8" and 1.13 * qb * kb <= 30.0 else 1)
-            out[name] = N.attn_kernel_name(lk, kw.get("softmax_scale"), kw["norm_bounds"], kw.get("prescaled", False), fp8)
+            pre = kw.get("prescaled", False)
+            if name == "self" and self._k_slots(kw) is not None and self.cp_group is None:
+                pre = 2
+            out[name] = N.attn_kernel_name(lk, kw.get("softmax_scale"), kw["norm_bounds"], pre, fp8)
         return out
 
     def state_dict_keys(self) -> List[str]:
@@ -678,10 +696,14 @@ class MinimalV1LVGDiT:
                 if cp is None or cp_size == 1:
                     qkv = self._proj(_rows(h, n * Bs), self.w_qkv[i], f"qkv.{i}")  # [n*Bs, 3D]
                     q_scale, attn_kw = self._self_attn_mode(i, hd)
+                    kslots = self._k_slots(attn_kw)
                     N.head_rmsnorm_rope(qkv, n_rows=n * Bs, B=Bs, H=H, head_off=0,
                                         weight=p[pre + "self_attn.q_norm.weight"], cos=cos, sin=sin, out_scale=q_scale)
                     N.head_rmsnorm_rope(qkv, n_rows=n * Bs, B=Bs, H=H, head_off=D,
-                                        weight=p[pre + "self_attn.k_norm.weight"], cos=cos, sin=sin)
+                                        weight=p[pre + "self_attn.k_norm.weight"], cos=cos, sin=sin,
+                                        **({} if kslots is None else dict(norm_max=kslots)))
+                    if kslots is not None:
+                        attn_kw = dict(attn_kw, k_norm_slots=kslots)
                     q = qkv.view(n, Bs, 3 * D)[:, :, :D].view(n, Bs, H, hd).transpose(0, 1)
                     kk = qkv.view(n, Bs, 3 * D)[:, :, D:2 * D].view(n, Bs, H, hd).transpose(0, 1)
                     vv = qkv.view(n, Bs, 3 * D)[:, :, 2 * D:].view(n, Bs, H, hd).transpose(0, 1)

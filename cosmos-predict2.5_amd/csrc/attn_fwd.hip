@@ -91,6 +91,8 @@ struct AttnArgs {
   float* lse_part;  // nsplit > 1: [nsplit][B][H][Lq] fp32 log2-sum-exp2 of the scaled scores
   float scale_log2; // softmax scale * log2(e) (1 for a pre-scaled q)
   float kbound;     // > 0: upper bound of |k| over all keys (fixed shift where it allows); 0: online max only
+  const float* kslots;  // gated pair: max |k| over all keys = the max of n_kslots floats kslots[32 i] (device memory)
+  int n_kslots;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -159,8 +161,13 @@ constexpr int kOStr = 272;                          // staged O row stride (256 
 constexpr int kQSlot = kQRows * kOStr;              // per wave 8704 B: next-block Q fragments (8 KiB) / staged O rows
 constexpr int kLdsP = kLds16 + kWaves * kQSlot;     // 143360
 
-// kMode: 0 fixed shift, 1 fixed shift known to be 0 (pre-scaled q, bound product <= 96: no initial C), 2 online
-template <int kKind, bool kPre, int kMode, bool kPersist = false>
+// kMode: 0 fixed shift, 1 fixed shift known to be 0 (pre-scaled q, bound product <= 96: no initial C), 2 online.
+// kGate (cp25_attn_fwd_prescaled_kslots: a data-tight key bound in device memory, the max |k| the producing RMSNorm
+// kernel measured): the same grid is launched twice, kGate 1 with kMode 1 and kGate 2 with kMode 2; a workgroup
+// whose query block's bound max|q_row| max|k| is <= 96 runs in the first launch (no shift, the fast loop) and exits
+// at once in the second, any other runs in the second (online max). Each block's arithmetic is exactly that of its
+// mode; which mode a row gets depends on the other rows of its 256-row block.
+template <int kKind, bool kPre, int kMode, bool kPersist = false, int kGate = 0>
 __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[kPersist ? kLdsP : kLds16];
   constexpr int KB1 = kKBuf16, VB0 = 2 * kKBuf16;
@@ -208,6 +215,37 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
     const unsigned short* src = qp + (int64_t)min(q_row[qh], a.Lq - 1) * a.q_sl + 8 * g;
 #pragma unroll
     for (int s = 0; s < 4; ++s) qf[qh][s] = *reinterpret_cast<const bf16x8*>(src + 32 * s);
+  }
+
+  if constexpr (kGate != 0) {
+    static_assert(kPre && !kPersist && ((kGate == 1 && kMode == 1) || (kGate == 2 && kMode == 2)), "gated pair");
+    __shared__ float gate_max[kWaves];
+    float km = lane < a.n_kslots ? a.kslots[32 * lane] : 0.f;  // max |k| over all keys (slots 128 B apart)
+    float qm = 0.f;                                      // max |q_row| over this wave's rows
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      float qq = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = static_cast<float>(qf[qh][s][e]);
+          qq = fmaf(x, x, qq);
+        }
+      qm = fmaxf(qm, sqrtf(group4_sum(qq)));
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      km = fmaxf(km, __shfl_xor(km, m));
+      qm = fmaxf(qm, __shfl_xor(qm, m));
+    }
+    if (lane == 0) gate_max[wave] = qm;
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) qm = fmaxf(qm, gate_max[w]);
+    // bound product with a 1e-3 margin (fp32 sums of the scores and of the norms); no slots written: online
+    const bool zero_ok = km > 0.f && qm * km * 1.001f <= kTop;
+    if (zero_ok != (kGate == 1)) return;  // uniform over the workgroup
   }
 
   f32x4 o[8][2];
@@ -1100,7 +1138,7 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
                        const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
                        const int64_t* o_strides, float softmax_scale, float q_norm_bound, float k_norm_bound,
                        int n_split, void* workspace, size_t ws_bytes, hipStream_t stream, bool prescaled = false,
-                       int fp8 = 0, const float* v_amax = nullptr) {
+                       int fp8 = 0, const float* v_amax = nullptr, const float* kslots = nullptr, int n_kslots = 0) {
   const bool fp8qk = fp8 >= 1;
   if (D != kD) return CP25_ERR_DTYPE;
   if (fp8qk && !prescaled) return CP25_ERR_INVAL;
@@ -1155,6 +1193,8 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
   a.lse_part = n_split > 1 ? (float*)workspace + (size_t)n_split * rows * kD : nullptr;
   a.scale_log2 = prescaled ? 1.f : softmax_scale * 1.4426950408889634f;
   a.kbound = q_norm_bound > 0.f ? k_norm_bound : 0.f;  // a missing q bound: online (the kernel measures |q_row|)
+  a.kslots = kslots;
+  a.n_kslots = n_kslots;
   const int64_t nwg = (int64_t)a.nqb * B * H * n_split;
   if (nwg > 0x7fffffff) return CP25_ERR_INVAL;
   const bool xk = Lk <= 4096;  // short-key launches (text cross-attention) get their own symbol in profiles
@@ -1166,7 +1206,13 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
     const int mode = m16_mode(q_norm_bound, k_norm_bound, a.scale_log2, prescaled);
     void (*kern)(AttnArgs) = nullptr;
     int64_t grid = nwg;
-    if (use_xattn_persistent(xk, n_split, mode, ntiles)) {
+    if (prescaled && kslots && mode != 1) {
+      // the gated pair: blocks whose data-tight bound allows it run the zero-shift loop, the others the online max
+      hipLaunchKernelGGL((xk ? attn_fwd_m16<1, true, 1, false, 1> : attn_fwd_m16<0, true, 1, false, 1>),
+                         dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
+      CP25_LAUNCH_CHECK();
+      kern = xk ? attn_fwd_m16<1, true, 2, false, 2> : attn_fwd_m16<0, true, 2, false, 2>;
+    } else if (use_xattn_persistent(xk, n_split, mode, ntiles)) {
       // one workgroup per CU over contiguous runs of blocks (every workgroup gets at least one)
       grid = std::min<int64_t>(nwg, num_cus());
       if (prescaled) kern = mode == 2 ? attn_fwd_m16<1, true, 2, true> : attn_fwd_m16<1, true, 1, true>;
@@ -1256,8 +1302,22 @@ extern "C" int cp25_attn_fwd_prescaled(const void* q, const void* k, const void*
                      q_norm_bound, k_norm_bound, n_split, workspace, ws_bytes, stream, true);
 }
 
+extern "C" int cp25_attn_fwd_prescaled_kslots(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq,
+                                              int Lk, int D, const int64_t* q_strides, const int64_t* k_strides,
+                                              const int64_t* v_strides, const int64_t* o_strides, float q_norm_bound,
+                                              float k_norm_bound, const float* k_norm_slots, int n_slots, int n_split,
+                                              void* workspace, size_t ws_bytes, hipStream_t stream) {
+  if (!k_norm_slots || n_slots < 1 || n_slots > 64 || ((uintptr_t)k_norm_slots & 3)) return CP25_ERR_INVAL;
+  return attn_launch(q, k, v, o, B, H, Lq, Lk, D, q_strides, k_strides, v_strides, o_strides, 0.6931471805599453f,
+                     q_norm_bound, k_norm_bound, n_split, workspace, ws_bytes, stream, true, 0, nullptr, k_norm_slots,
+                     n_slots);
+}
+
 extern "C" const char* cp25_attn_kernel(int Lk, float softmax_scale, float q_norm_bound, float k_norm_bound,
                                         int prescaled, int fp8) {
+  if (prescaled == 2 && m16_mode(q_norm_bound, k_norm_bound, 1.f, true) != 1)  // cp25_attn_fwd_prescaled_kslots
+    return Lk <= 4096 ? "attn_fwd_m16<cross, prescaled, gated zero shift | online max>"
+                      : "attn_fwd_m16<self, prescaled, gated zero shift | online max>";
   if (fp8 == 2) return Lk <= 4096 ? "attn_fwd_f8<cross, fp8 Q K^T + fp8 P.V>" : "attn_fwd_f8<self, fp8 Q K^T + fp8 P.V>";
   if (fp8 == 1) return Lk <= 4096 ? "attn_fwd_f8<cross, fp8 Q K^T>" : "attn_fwd_f8<self, fp8 Q K^T>";
   if (Lk <= 4096) {

@@ -192,13 +192,23 @@ __global__ void __launch_bounds__(256) final_ln_mod_kernel(
 
 // ---------------------------------------------------------------- per-head RMSNorm (+ RoPE)
 // 16 lanes per (row, head) of 128 elements; lane i holds elements 8i .. 8i+7.
+// kNmax: also the max |output row| over all (row, head) items into nmax[64 x 32] (atomic max on the float bits into
+// slot blockIdx % 64 at float index 32 slot, one atomic per workgroup; the caller zeroes the slots): the data-tight
+// key bound of the gated attention
+template <bool kNmax = false>
 __global__ void __launch_bounds__(256) head_rmsnorm_rope_kernel(
     unsigned short* __restrict__ buf, int64_t row_stride, int64_t n_rows, int B, int H, int head_off,
     const unsigned short* __restrict__ w, const float* __restrict__ cosb, const float* __restrict__ sinb,
-    unsigned short* __restrict__ out2, int64_t out2_stride, float eps, float out_scale) {
-  const int64_t item = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);  // (row, head)
+    unsigned short* __restrict__ out2, int64_t out2_stride, float eps, float out_scale,
+    unsigned int* __restrict__ nmax = nullptr) {
+  int64_t item = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);  // (row, head)
   const int li = threadIdx.x & 15;
-  if (item >= n_rows * H) return;
+  const bool valid = item < n_rows * H;
+  if constexpr (!kNmax) {
+    if (!valid) return;
+  } else {
+    item = valid ? item : n_rows * H - 1;  // the wave reduction below needs every lane; extra lanes redo the last item
+  }
   const int64_t row = item / H;
   const int h = (int)(item % H);
   unsigned short* p = buf + row * row_stride + head_off + h * 128 + li * 8;
@@ -234,8 +244,26 @@ __global__ void __launch_bounds__(256) head_rmsnorm_rope_kernel(
   u16x8 o;
 #pragma unroll
   for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e] * out_scale);  // out_scale 1: exact, the reference's rounding
-  *reinterpret_cast<u16x8*>(p) = o;
-  if (out2 != nullptr) *reinterpret_cast<u16x8*>(out2 + row * out2_stride + h * 128 + li * 8) = o;
+  if constexpr (kNmax) {
+    float nn = 0.f;  // |row|^2 of the bf16 values written (the ones the attention reads)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) nn = fmaf(bf2f(o[e]), bf2f(o[e]), nn);
+#pragma unroll
+    for (int m = 8; m >= 1; m >>= 1) nn += __shfl_xor(nn, m, 16);  // the item's 16 lanes
+    nn = fmaxf(nn, __shfl_xor(nn, 16));                             // the wave's 4 items
+    nn = fmaxf(nn, __shfl_xor(nn, 32));
+    __shared__ float wmax[4];
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = nn;
+    __syncthreads();
+    // one atomic per workgroup, into one of 64 slots a cache line apart (all slots in one line serialised the
+    // atomics of the whole launch on one L2 channel: ~3.5 ms per launch at the DiT shape)
+    if (threadIdx.x == 0)
+      atomicMax(nmax + (blockIdx.x & 63) * 32, __float_as_uint(sqrtf(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3])))));
+  }
+  if (!kNmax || valid) {
+    *reinterpret_cast<u16x8*>(p) = o;
+    if (out2 != nullptr) *reinterpret_cast<u16x8*>(out2 + row * out2_stride + h * 128 + li * 8) = o;
+  }
 }
 
 // plain strided copy of a [rows, width] bf16 block (K/V export for the CP all-gather)
@@ -417,12 +445,26 @@ extern "C" int cp25_head_rmsnorm_rope_scaled(void* buf, int64_t row_stride, int6
                                              int head_off, const void* weight, const float* cos_tab,
                                              const float* sin_tab, void* out2, int64_t out2_stride, float eps,
                                              float out_scale, hipStream_t stream) {
+  return cp25_head_rmsnorm_rope_nmax(buf, row_stride, n_rows, B, H, head_off, weight, cos_tab, sin_tab, out2,
+                                     out2_stride, eps, out_scale, nullptr, stream);
+}
+
+extern "C" int cp25_head_rmsnorm_rope_nmax(void* buf, int64_t row_stride, int64_t n_rows, int B, int H, int head_off,
+                                           const void* weight, const float* cos_tab, const float* sin_tab, void* out2,
+                                           int64_t out2_stride, float eps, float out_scale, float* norm_max_slots,
+                                           hipStream_t stream) {
   if (!buf || !weight || n_rows <= 0 || H <= 0 || B <= 0) return CP25_ERR_INVAL;
   if ((row_stride % 8) || (head_off % 8) || ((cos_tab == nullptr) != (sin_tab == nullptr))) return CP25_ERR_INVAL;
+  if ((uintptr_t)norm_max_slots & 3) return CP25_ERR_INVAL;
   const int64_t items = n_rows * H;
-  hipLaunchKernelGGL(head_rmsnorm_rope_kernel, dim3((unsigned)cdiv(items, 16)), dim3(256), 0, stream,
-                     (unsigned short*)buf, row_stride, n_rows, B, H, head_off, (const unsigned short*)weight, cos_tab,
-                     sin_tab, (unsigned short*)out2, out2_stride, eps, out_scale);
+  if (norm_max_slots)
+    hipLaunchKernelGGL(head_rmsnorm_rope_kernel<true>, dim3((unsigned)cdiv(items, 16)), dim3(256), 0, stream,
+                       (unsigned short*)buf, row_stride, n_rows, B, H, head_off, (const unsigned short*)weight, cos_tab,
+                       sin_tab, (unsigned short*)out2, out2_stride, eps, out_scale, (unsigned int*)norm_max_slots);
+  else
+    hipLaunchKernelGGL(head_rmsnorm_rope_kernel<false>, dim3((unsigned)cdiv(items, 16)), dim3(256), 0, stream,
+                       (unsigned short*)buf, row_stride, n_rows, B, H, head_off, (const unsigned short*)weight, cos_tab,
+                       sin_tab, (unsigned short*)out2, out2_stride, eps, out_scale, nullptr);
   CP25_LAUNCH_CHECK();
   return CP25_OK;
 }

@@ -75,6 +75,20 @@ int cp25_attn_fwd_prescaled(const void* q, const void* k, const void* v, void* o
                             const int64_t* o_strides, float q_norm_bound, float k_norm_bound, int n_split,
                             void* workspace, size_t ws_bytes, hipStream_t stream);
 
+/* cp25_attn_fwd_prescaled with a data-tight key bound in device memory: the max of k_norm_slots[32 i], i < n_slots
+ * (n_slots <= 64; the [64][32] buffer cp25_head_rmsnorm_rope_nmax filled on k) bounds |k| over all keys. Where the host bounds already
+ * allow the zero shift (product <= 96) this is cp25_attn_fwd_prescaled. Otherwise the same grid is launched twice
+ * (stream-ordered, no host synchronisation): a 256-query block whose own bound max|q_row| max|k| is <= 96 runs the
+ * zero-shift loop in the first launch, any other block the online max in the second, so trained q/k norm weights
+ * (whose weight-based bounds exceed 96) keep the fast loop wherever the data allows. A row's mode depends on its
+ * block, so context-parallel shards must not use this form when they need bit-identical rows. Same reference op as
+ * cp25_attn_fwd_bounded. */
+int cp25_attn_fwd_prescaled_kslots(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq, int Lk,
+                                   int D, const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
+                                   const int64_t* o_strides, float q_norm_bound, float k_norm_bound,
+                                   const float* k_norm_slots, int n_slots, int n_split, void* workspace,
+                                   size_t ws_bytes, hipStream_t stream);
+
 /* dst[r, c] = OCP e4m3(bf16 src[r, c] * scale) (saturated to +-448, round to nearest even), row strides in
  * elements; width % 16 == 0. The fixed-scale fp8 copies of q and k for cp25_attn_fwd_prescaled_fp8qk. */
 int cp25_cast_fp8_e4m3(const void* src, int64_t src_stride, void* dst, int64_t dst_stride, int64_t n_rows,
@@ -113,7 +127,8 @@ int cp25_attn_fwd_prescaled_fp8(const void* q8, const void* k8, const void* v8t,
                                 const int64_t* o_strides, float q_norm_bound, float k_norm_bound, int n_split,
                                 void* workspace, size_t ws_bytes, hipStream_t stream);
 
-/* Name of the kernel form cp25_attn_fwd_bounded (prescaled = 0, fp8 = 0), _prescaled (prescaled = 1),
+/* Name of the kernel form cp25_attn_fwd_bounded (prescaled = 0, fp8 = 0), _prescaled (prescaled = 1), _prescaled_kslots
+ * (prescaled = 2),
  * _prescaled_fp8qk (fp8 = 1) or _prescaled_fp8 (fp8 = 2) launches for these arguments (a static string), e.g.
  * "attn_fwd_m16<self, prescaled, online max>": what a bench or log reports as the kernel that ran. */
 const char* cp25_attn_kernel(int Lk, float softmax_scale, float q_norm_bound, float k_norm_bound, int prescaled,
@@ -177,6 +192,16 @@ int cp25_head_rmsnorm_rope(void* buf, int64_t row_stride, int64_t n_rows, int B,
 int cp25_head_rmsnorm_rope_scaled(void* buf, int64_t row_stride, int64_t n_rows, int B, int H, int head_off,
                                   const void* weight, const float* cos_tab, const float* sin_tab, void* out2,
                                   int64_t out2_stride, float eps, float out_scale, hipStream_t stream);
+
+/* cp25_head_rmsnorm_rope_scaled that also measures the result: the 64 slots norm_max_slots[32 i] (a float [64][32]
+ * buffer in device memory, zeroed by the caller; slots one 128-B line apart so the atomics spread over L2 channels)
+ * receive, by atomic max, the largest |row| (L2 norm over a head's 128 bf16 values as written) of the call (the max
+ * of the 64 is the max over all rows and heads). For k, that is the data-tight key bound
+ * cp25_attn_fwd_prescaled_kslots reads; NULL slots: cp25_head_rmsnorm_rope_scaled. */
+int cp25_head_rmsnorm_rope_nmax(void* buf, int64_t row_stride, int64_t n_rows, int B, int H, int head_off,
+                                const void* weight, const float* cos_tab, const float* sin_tab, void* out2,
+                                int64_t out2_stride, float eps, float out_scale, float* norm_max_slots,
+                                hipStream_t stream);
 
 /* dst[r, 0:width] = src[r, 0:width] for bf16 rows (K/V export before the CP all-gather). */
 int cp25_copy_rows(const void* src, int64_t src_stride, void* dst, int64_t dst_stride, int64_t n_rows, int64_t width,

@@ -31,7 +31,7 @@ def test_no_lds_read_races(src):
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="hipcc not installed")
 def test_self_attention_loop_shape():
-    rep = isa_check.check(os.path.join(CSRC, "attn_fwd.hip"), "attn_fwd_m16ILi0ELb1ELi1ELb0E")
+    rep = isa_check.check(os.path.join(CSRC, "attn_fwd.hip"), "attn_fwd_m16ILi0ELb1ELi1ELb0ELi0E")
     (r,) = rep.values()  # the bench's kernel: self-attention, prescaled q, zero shift
     assert r["inloop_scratch"] == 0
     assert r["nops"] <= 40, r["nops"]  # 192 with the operand-redefining wait pins
