@@ -237,26 +237,13 @@ constexpr int kBuf8 = 4 * kHalf;      // A0 A1 B0 B1
 // (k bytes 16 g .. and 64 + 16 g ..: the same k slots in A and B, which is all the sum needs) instead of two bf16
 // MFMAs: twice the cycles each, half the count, twice the K -- 2x the bf16 rate. The epilogue multiplies each
 // accumulator by a_scale[row] * w_scale[col] before the bf16 rounding (torch._scaled_mm's definition).
-// GELU epilogue by table: the layer1 product is rounded to bf16 before the GELU, so GELU's bf16 result is a function of
-// 16 input bits. gelu_tab holds bf16(gelu_erf(x)) for both signs and |x| in [2^-16, 8) (binary exponents 111 .. 129:
-// 2 x 19 x 128 entries, 9.5 KiB of LDS, filled by each workgroup from the same gelu_erf): one LDS read per element
-// instead of ~25 VALU operations (three of them transcendental), bit-identical; a wave with any input outside the
-// table's range (|x| < 2^-16 or >= 8: rare) evaluates gelu_erf for those lanes.
-constexpr int kGeluE0 = 111, kGeluNE = 19;
-constexpr int kGeluTab = 2 * kGeluNE * 128;  // entries
-__device__ __forceinline__ int gelu_tab_index(unsigned u) {  // u: bf16 bits; -1 outside the table
-  const unsigned e = ((u >> 7) & 0xffu) - (unsigned)kGeluE0;
-  return e < (unsigned)kGeluNE ? (int)((u >> 15) * (kGeluNE * 128) + e * 128 + (u & 127u)) : -1;
-}
-
 template <int kEpi, int kES = 2>
 __global__ void __launch_bounds__(kThreads, 1)
 gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned short* __restrict__ W, int64_t ldw,
             unsigned short* __restrict__ C, int64_t ldc, int M, int N, int K, ResEpi re, const float* __restrict__ a_scale,
             const float* __restrict__ w_scale) {
   // fp8: 2 KiB past the K-tile buffers / C tile hold the tile's 256 row scales of A and 256 column scales of W
-  __shared__ __attribute__((aligned(16)))
-  char smem[2 * kBuf8 + (kES == 1 ? 2048 : 0) + (kEpi == CP25_EPI_GELU ? 2 * kGeluTab : 0)];
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf8 + (kES == 1 ? 2048 : 0)];
   static_assert(kES == 1 || kES == 2, "bf16 (2) or fp8 (1) operands");
   typedef int i32x8 __attribute__((ext_vector_type(8)));
 
@@ -411,15 +398,6 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
 
   int tile = my_slot;
   if (tile >= n_tiles) return;
-  if constexpr (kEpi == CP25_EPI_GELU) {  // the GELU table (visible after the prologue's barrier)
-    unsigned short* tab = reinterpret_cast<unsigned short*>(smem + 2 * kBuf8);
-    for (int i = tid; i < kGeluTab; i += kThreads) {
-      const int r = i % (kGeluNE * 128);
-      const unsigned u = (unsigned)(i / (kGeluNE * 128)) << 15 | (unsigned)(kGeluE0 + r / 128) << 7 | (unsigned)(r % 128);
-      tab[i] = f2bf(gelu_exact(bf2f((unsigned short)u)));
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  }
   int m0, n0;
   tile_mn(tile, m0, n0);
   set_tile(m0, n0);
@@ -490,18 +468,9 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
                 const f32x4_t as = *reinterpret_cast<const f32x4_t*>(sc + mq * 128 + wr * 64 + 16 * i + 4 * fg);
                 a = a * as[r] * sc[256 + nq * 128 + wc * 32 + 16 * j + fr];
               }
-              if constexpr (kEpi == CP25_EPI_GELU) {
-                const unsigned short u = f2bf(a);
-                const int ti = gelu_tab_index(u);
-                unsigned short g = reinterpret_cast<const unsigned short*>(smem + 2 * kBuf8)[ti < 0 ? 0 : ti];
-                if (__builtin_expect(__any(ti < 0), 0)) {
-                  const unsigned short gs = f2bf(gelu_exact(bf2f(u)));
-                  g = ti < 0 ? gs : g;
-                }
-                stj[j][(mq * 128 + 16 * i + r) * 256 + nq * 128] = g;
-              } else {
-                stj[j][(mq * 128 + 16 * i + r) * 256 + nq * 128] = f2bf(rbf(a));
-              }
+              float y = rbf(a);
+              if constexpr (kEpi == CP25_EPI_GELU) y = gelu_exact(y);
+              stj[j][(mq * 128 + 16 * i + r) * 256 + nq * 128] = f2bf(y);
             }
     // (after the accumulators are in the LDS: their registers hold the x / gate chunks)
     // thread t owns rows m0 + 16 it + t / 32 (it = 0..15), 16-B chunk t % 32 of the C tile
