@@ -593,11 +593,8 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
     auto issue = [&](auto NC) __attribute__((always_inline)) { issue_pair(PAR, NC); };
     constexpr auto nreads = [](int n) constexpr { return n >= 32 ? 0 : (n >= 16 ? 1 : 2); };
     __builtin_amdgcn_s_setprio(1);
-    // group B's first kAhead pairs are in flight (PRE): the loop's counted waits retire them
-    if constexpr (!decltype(PRE)::value) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      static_for<kAhead>(issue);
-    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (!decltype(PRE)::value) static_for<kAhead>(issue);
     static_for<32>([&](auto NC) __attribute__((always_inline)) {
       constexpr int n = decltype(NC)::value;
       issue(std::integral_constant<int, n + kAhead>{});
@@ -660,11 +657,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
       softmax(t);
       if (t + 2 < ntiles) load_tile(t + 3);
       static_for<kAhead>([&](auto NC) __attribute__((always_inline)) { issue_pair(PAR, NC); });
-      // a raw barrier behind a counted wait: the K(t+2) writes retire, the kAhead pairs' reads just issued stay in
-      // flight across it (a __syncthreads() fence waited for them too, before the barrier, on the longer phase)
-      asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(2 * kAhead) : "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
+      __syncthreads();
       mfma_phase(PAR, std::true_type{});
       __syncthreads();
     };
