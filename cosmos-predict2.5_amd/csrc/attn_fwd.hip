@@ -563,7 +563,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
   if (!group_b) softmax(0);
   __syncthreads();
 
-  // one MFMA phase: P.V of tile t then Q K^T of tile t+1 (64 MFMAs of 16 cycles) + the 4 row-sum MFMAs. Operand pair
+  // one MFMA phase: the 4 row-sum MFMAs, P.V of tile t, then Q K^T of tile t+1 (64 MFMAs of 16 cycles). Operand pair
   // n (one fragment, two MFMAs, one per query half): n < 16 the V^T fragment (db = n & 7, ks = n >> 3, two
   // transposed reads), n >= 16 the K fragment (kb = (n - 16) & 3, s = (n - 16) >> 2). (The Q K^T after the last tile
   // reads a stale K buffer; its scores are never used.)
@@ -598,6 +598,13 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       static_for<kAhead>(issue);
     }
+    // row sums of P(t) first: they need no LDS operand, so they cover the first operand reads' latency (after the
+    // P.V pairs they measured 0.25 % slower, profiles/r3/attn_nop/barrier_rowsum_ab.log)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) lsum[qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones8, pb[ks][qh], lsum[qh], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
     static_for<32>([&](auto NC) __attribute__((always_inline)) {
       constexpr int n = decltype(NC)::value;
       issue(std::integral_constant<int, n + kAhead>{});
@@ -622,12 +629,6 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
         } else {
           o[n & 7][qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[n % kR], pb[n >> 3][qh], o[n & 7][qh], 0, 0, 0);
         }
-      }
-      if constexpr (n == 15) {  // row sums of P(t), after its P.V pairs
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-          for (int qh = 0; qh < 2; ++qh) lsum[qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones8, pb[ks][qh], lsum[qh], 0, 0, 0);
       }
       // program order = issue order (the scheduler otherwise sinks MFMAs below later reads and renames accumulators)
       __builtin_amdgcn_sched_barrier(0);

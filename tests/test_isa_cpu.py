@@ -33,5 +33,7 @@ def test_no_lds_read_races(src):
 def test_self_attention_loop_shape():
     rep = isa_check.check(os.path.join(CSRC, "attn_fwd.hip"), "attn_fwd_m16ILi0ELb1ELi1ELb0ELi0E")
     (r,) = rep.values()  # the bench's kernel: self-attention, prescaled q, zero shift
-    assert r["inloop_scratch"] == 0
+    # scratch traffic only in the loop's cold contract-guard branch (a NaN poison of overflowed rows), never in the
+    # MFMA / softmax phases: at most the one reload + one spill of the NaN fill
+    assert r["inloop_scratch"] <= 2, r["inloop_scratch"]
     assert r["nops"] <= 40, r["nops"]  # 192 with the operand-redefining wait pins

@@ -3,7 +3,7 @@ block boundary, for same-box A/B with tools/bench_xattn.py --lib; results are WR
 The product source is not touched: the patched copy is compiled from /tmp and linked with the in-tree objects.
 usage: python tools/lab/attn_variant.py <name> <patch>[,<patch>...]  ->  tools/lab/libcp25_<name>.so
 patches: nostore (no O stores at block boundaries), nodma (no next-block Q copy), noqread (no Q read from LDS),
-nostagger (the Q copy at tile 0 in every workgroup; correct results), none"""
+nostagger (the Q copy at tile 0 in every workgroup; correct results), rowsum_first (correct results), none"""
 import os
 import subprocess
 import sys
@@ -20,6 +20,21 @@ PATCHES = {
     "noqread": [("      if (t == ntk - 1 && blk0 + tb + 1 < blk_end) {\n",
                  "      if (t == ntk - 1 && blk0 + tb + 1 < 0) {\n")],
     "nostagger": [("constexpr bool kQCopyStagger = true;\n", "constexpr bool kQCopyStagger = false;\n")],  # correct
+    # the 4 row-sum MFMAs at the start of the MFMA phase (they need no LDS operand: they cover the first reads' latency)
+    # instead of after the P.V pairs; correct results
+    "rowsum_first": [("      if constexpr (n == 15) {  // row sums of P(t), after its P.V pairs\n",
+                      "      if constexpr (n == 99) {  // row sums of P(t), after its P.V pairs\n"),
+                     ("""      static_for<kAhead>(issue);
+    }
+    static_for<32>([&](auto NC) __attribute__((always_inline)) {""",
+                      """      static_for<kAhead>(issue);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) lsum[qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones8, pb[ks][qh], lsum[qh], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<32>([&](auto NC) __attribute__((always_inline)) {""")],
     "none": [],
 }
 

@@ -466,22 +466,6 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
     // Element (row, col): row = mq 128 + wr 64 + 16 i + 4 fg + r, col = nq 128 + wc 32 + 16 j + fr; the lane part
     // of the address has two values (j = 0, 1), the rest is an immediate. The bases are laundered per tile so the
     // compiler does not hoist them out of the tile loop (they would stay live across the K loop).
-    // CP25_EPI_RES: this thread's 16 x chunks are requested first, into the registers the K loop's fragments held,
-    // so their HBM latency runs under the staging below (requested after it, they waited out the whole latency at
-    // the combine); the 16 gate chunks (L2-resident, one row per frame) follow the staging as before.
-    // thread t owns rows m0 + 16 it + t / 32 (it = 0..15), 16-B chunk t % 32 of the C tile
-    const int ch = tid & 31, r0 = tid >> 5;
-    u32x4 xres[16], gres[16];
-    if constexpr (kEpi == CP25_EPI_RES) {
-      const int row_a = min(m0 + r0, M - 1), tok_a = row_a / re.B, b = row_a % re.B, dtok = 16 / re.B;
-      const unsigned short* xp = re.x + (int64_t)tok_a * re.x_st + b * re.x_sb + n0 + ch * 8;
-      const int n_valid = (M - 1 - row_a) / 16;  // rows row_a + 16 it, it <= n_valid, exist
-      // the row offset is selected arithmetically (x 0 or 1): a selected POINTER made the compiler load the fallback
-      // row first and branch around a second load behind a vmcnt(0) -- sixteen serialised HBM round trips per tile
-#pragma unroll
-      for (int it = 0; it < 16; ++it)
-        xres[it] = *reinterpret_cast<const u32x4*>(xp + (int64_t)(it * dtok) * re.x_st * (int64_t)(it <= n_valid));
-    }
     int ez = 0;
     asm volatile("" : "+v"(ez));
     unsigned short* const ct = reinterpret_cast<unsigned short*>(smem);
@@ -519,19 +503,24 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
                 stj[j][(mq * 128 + 16 * i + r) * 256 + nq * 128] = f2bf(rbf(a));
               }
             }
-    // (after the accumulators are in the LDS: their registers hold the gate chunks)
+    // (after the accumulators are in the LDS: their registers hold the x / gate chunks)
+    // thread t owns rows m0 + 16 it + t / 32 (it = 0..15), 16-B chunk t % 32 of the C tile
+    const int ch = tid & 31, r0 = tid >> 5;
+    u32x4 xres[16], gres[16];
     if constexpr (kEpi == CP25_EPI_RES) {
       // row r0 + 16 it: token tok_a + it * (16 / B), batch entry b (16 % B == 0), frame by a running remainder that
       // wraps at most once per step (16 / B <= hw, host-checked): straight-line code. Rows past M (a ragged last
       // row-tile) read the thread's first valid row instead (their results are not stored).
       const int row_a = min(m0 + r0, M - 1), tok_a = row_a / re.B, b = row_a % re.B, dtok = 16 / re.B;
       int64_t fr = (re.tok0 + tok_a) / re.hw, rem = (re.tok0 + tok_a) % re.hw;
+      const unsigned short* xp = re.x + (int64_t)tok_a * re.x_st + b * re.x_sb + n0 + ch * 8;
       const unsigned short* gp = re.gate + b * re.g_sb + n0 + ch * 8;
       const int n_valid = (M - 1 - row_a) / 16;  // rows row_a + 16 it, it <= n_valid, exist
 #pragma unroll
       for (int it = 0; it < 16; ++it) {
         const bool ok = it <= n_valid;
-        gres[it] = *reinterpret_cast<const u32x4*>(gp + fr * re.g_st * (int64_t)ok);
+        xres[it] = *reinterpret_cast<const u32x4*>(ok ? xp + (int64_t)it * dtok * re.x_st : xp);
+        gres[it] = *reinterpret_cast<const u32x4*>(ok ? gp + fr * re.g_st : gp);
         rem += dtok;
         const bool wrap = rem >= re.hw;
         rem -= wrap ? re.hw : 0;

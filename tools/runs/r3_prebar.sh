@@ -1,6 +1,7 @@
 #!/bin/bash
 # round 3 (session 2): group B's pre-issued operand reads kept in flight across its barrier (raw barrier behind a
-# counted lgkmcnt) vs the previous build (tools/lab/attn_fwd_prebar.hip): attention tests, same-box A/B
+# counted lgkmcnt) vs the previous build (tools/lab/attn_fwd_prebar.hip), and the row-sum MFMAs first in the MFMA phase
+# (tools/lab/attn_variant.py rowsum_first): attention tests, same-box A/B
 set -o pipefail
 export PYTHONUNBUFFERED=1
 mkdir -p gpurun_out/r3pb
@@ -8,7 +9,7 @@ timeout -k 10 900 python -u -m pytest tests/test_attn_m16_gpu.py tests/test_atte
 tail -1 gpurun_out/r3pb/tests.log
 A="--L 109120 --B 2 --H 16 --fused --bounded --prescaled --iters 6"
 for pass in 1 2 3; do
-  for v in product prebar; do
+  for v in product prebar rowsum_first; do
     lib=""; [ $v != product ] && lib=tools/lab/libcp25_$v.so
     timeout -k 10 120 python tools/bench_attn.py $A ${lib:+--lib $lib} 2>gpurun_out/r3pb/err.log >> gpurun_out/r3pb/self_ab.log || { tail gpurun_out/r3pb/err.log; exit 1; }
   done
