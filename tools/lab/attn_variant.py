@@ -3,7 +3,9 @@ block boundary, for same-box A/B with tools/bench_xattn.py --lib; results are WR
 The product source is not touched: the patched copy is compiled from /tmp and linked with the in-tree objects.
 usage: python tools/lab/attn_variant.py <name> <patch>[,<patch>...]  ->  tools/lab/libcp25_<name>.so
 patches: nostore (no O stores at block boundaries), nodma (no next-block Q copy), noqread (no Q read from LDS),
-nostagger (the Q copy at tile 0 in every workgroup; correct results), rowsum_first (correct results), none"""
+nostagger (the Q copy at tile 0 in every workgroup; correct results), rowsum_first (correct results),
+prio_b_hold, prio_static_b (wave priority forms; correct results), ahead2, ahead4 (operand ring depth;
+correct results), none"""
 import os
 import subprocess
 import sys
@@ -35,6 +37,26 @@ PATCHES = {
       for (int qh = 0; qh < 2; ++qh) lsum[qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones8, pb[ks][qh], lsum[qh], 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
     static_for<32>([&](auto NC) __attribute__((always_inline)) {""")],
+    # wave priority: group B (waves 4-7, the later-dispatched half) stays at s_setprio 1 through its softmax phase
+    # (A still flips 1 / 0 per phase); or the guide's static form: no per-phase flips, group B at 1 from the start
+    "prio_b_hold": [("""    __builtin_amdgcn_s_setprio(0);
+  };
+  if (!group_b) {""", """    if (!group_b) __builtin_amdgcn_s_setprio(0);
+  };
+  if (!group_b) {""")],
+    "prio_static_b": [("""    __builtin_amdgcn_s_setprio(1);
+    // group B's first kAhead pairs""", """    // group B's first kAhead pairs"""),
+                      ("""    __builtin_amdgcn_s_setprio(0);
+  };
+  if (!group_b) {""", """  };
+  if (!group_b) {"""),
+                      ("""    // group B: phase 2t softmax(t) + K(t+2) staging, phase 2t+1 MFMA
+""", """    // group B: phase 2t softmax(t) + K(t+2) staging, phase 2t+1 MFMA
+    __builtin_amdgcn_s_setprio(1);
+""")],
+    # operand ring depth of the MFMA phase (pairs read ahead of their MFMAs; ring = depth + 1); correct results
+    "ahead2": [("constexpr int kAhead = 3;", "constexpr int kAhead = 2;")],
+    "ahead4": [("constexpr int kAhead = 3;", "constexpr int kAhead = 4;")],
     "none": [],
 }
 
