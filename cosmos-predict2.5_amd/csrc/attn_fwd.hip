@@ -131,7 +131,9 @@ struct AttnArgs {
 // The host picks the mode from the bounds (m16_mode).
 constexpr int kKStride16 = 288;
 constexpr int kVStride16 = 288;
-constexpr int kAhead = 3;  // MFMA phase: operand pairs read ahead of their MFMAs
+// MFMA phase: operand pairs read ahead of their MFMAs. 2 (ring of 3 fragments) frees 4 VGPRs against 3: the online
+// form -3.4 % per launch, zero shift -0.1 %, 4: online +7 % (profiles/r3/attn_nop/ring_depth_ab.log, ring_depth2_ab.log)
+constexpr int kAhead = 2;
 constexpr int kKBuf16 = kKBlk * kKStride16;        // 18432
 constexpr int kVBuf16 = kKBlk * kVStride16;        // 18432
 constexpr int kLds16 = 2 * kKBuf16 + 2 * kVBuf16;  // 73728

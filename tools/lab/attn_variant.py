@@ -4,7 +4,7 @@ The product source is not touched: the patched copy is compiled from /tmp and li
 usage: python tools/lab/attn_variant.py <name> <patch>[,<patch>...]  ->  tools/lab/libcp25_<name>.so
 patches: nostore (no O stores at block boundaries), nodma (no next-block Q copy), noqread (no Q read from LDS),
 nostagger (the Q copy at tile 0 in every workgroup; correct results), rowsum_first (correct results),
-prio_b_hold, prio_static_b (wave priority forms; correct results), ahead2, ahead4 (operand ring depth;
+prio_b_hold, prio_static_b (wave priority forms; correct results), ahead3, ahead4 (operand ring depth;
 correct results), none"""
 import os
 import subprocess
@@ -55,8 +55,8 @@ PATCHES = {
     __builtin_amdgcn_s_setprio(1);
 """)],
     # operand ring depth of the MFMA phase (pairs read ahead of their MFMAs; ring = depth + 1); correct results
-    "ahead2": [("constexpr int kAhead = 3;", "constexpr int kAhead = 2;")],
-    "ahead4": [("constexpr int kAhead = 3;", "constexpr int kAhead = 4;")],
+    "ahead3": [("constexpr int kAhead = 2;", "constexpr int kAhead = 3;")],
+    "ahead4": [("constexpr int kAhead = 2;", "constexpr int kAhead = 4;")],
     "none": [],
 }
 
