@@ -5,7 +5,7 @@ usage: python tools/lab/attn_variant.py <name> <patch>[,<patch>...]  ->  tools/l
 patches: nostore (no O stores at block boundaries), nodma (no next-block Q copy), noqread (no Q read from LDS),
 nostagger (the Q copy at tile 0 in every workgroup; correct results), rowsum_first (correct results),
 prio_b_hold, prio_static_b (wave priority forms; correct results), ahead3, ahead4 (operand ring depth;
-correct results), none"""
+correct results), hotload, noload (staging-load probes), none"""
 import os
 import subprocess
 import sys
@@ -57,6 +57,20 @@ PATCHES = {
     # operand ring depth of the MFMA phase (pairs read ahead of their MFMAs; ring = depth + 1); correct results
     "ahead3": [("constexpr int kAhead = 2;", "constexpr int kAhead = 3;")],
     "ahead4": [("constexpr int kAhead = 2;", "constexpr int kAhead = 4;")],
+    # staging-load probes of the self-attention loop (WRONG results): hotload = every tile's K/V load reads tile t & 1
+    # (L2-resident bytes: the HBM part of the load latency gone); noload = no K/V loads after the prologue
+    "hotload": [("      kt = t;\n", "      kt = t & 1;\n")],
+    "noload": [("""        softmax(t + 1);
+        load_tile(t + 2);
+      }
+      __syncthreads();
+    };
+    // pairs of tiles""", """        softmax(t + 1);
+        if (t < 0) load_tile(t + 2);
+      }
+      __syncthreads();
+    };
+    // pairs of tiles"""), ("      if (t + 2 < ntiles) load_tile(t + 3);\n", "      if (t < 0) load_tile(t + 3);\n")],
     "none": [],
 }
 
