@@ -1,0 +1,1378 @@
+// Flash-attention forward for the DiT self- and cross-attention (gfx950, bf16 in/out, head dim 128).
+//
+// Replaces the reference's attention op: cosmos_predict2/_src/predict2/networks/attention.py:90-181
+// (q/k/v recast to bf16, softmax(QK^T / sqrt(D)) V, no mask, no dropout, non-causal), which the DiT
+// calls through MinimalA2AAttnOp (networks/a2a_cp.py:208-219) on [B, S, H, D] tensors.
+//
+// Two kernels:
+//   attn_fwd_m16  every bf16 form. 8 waves x 32 query rows of one (b, h) per workgroup, v_mfma_f32_16x16x32_bf16,
+//                 ping-pong of the two waves of a SIMD (one runs its MFMA phase while the other runs its softmax),
+//                 K/V 64-key tiles double-buffered in padded LDS rows, counted-lgkmcnt operand ring, row sums by
+//                 MFMA, XCD-aware grid. The softmax shift of a query row enters as the initial C of its Q K^T MFMA
+//                 chains, so P = exp2(S) needs no per-score VALU beyond the exp (prescaled q). The shift is either
+//                 fixed from a norm bound (b_row = |q_row| max|k| <= 98: shift max(b_row - 96, 0), no max at all) or
+//                 an online row max with lazy rescale (any data; per wave, decided at the kernel start).
+//   attn_fwd_f8   the config-5 fp8 option (no reference counterpart): Q K^T on v_mfma_f32_32x32x64_f8f6f4 over e4m3
+//                 q / k, and with kF8 = 3 also P.V on e5m2 P (made without exp2) and e4m3 V^T tiles.
+// Archived variants and A/B switches of round 2 (one wave per SIMD, LDS-DMA staging, V^T tiles, persistent
+// cross-attention, 32x32x16 bf16 forms, lab isolation builds): tools/lab/attn_fwd_r2.hip.
+// NaN inputs are not supported (built with -fno-honor-nans; the reference's flash kernels do not define NaN
+// propagation either). Numerics: scores, shifts and sums fp32, P rounded to bf16 before P.V (as every flash kernel
+// the reference dispatches to does), O accumulated in fp32, normalised and rounded once to bf16.
+#include "cp25_common.h"
+
+#include <algorithm>
+#include <type_traits>
+
+namespace {
+
+constexpr int kD = 128;        // head dim
+constexpr int kWaves = 8;      // waves per workgroup
+constexpr int kQRows = 32;     // query rows per wave
+constexpr int kQBlk = kWaves * kQRows;  // 256 query rows per workgroup
+constexpr int kKBlk = 64;      // keys per tile
+constexpr int kThreads = kWaves * 64;
+// Softmax-shift ranges (log2 units). A term is 2^(s - shift); the row sum of up to ~1.4e5 keys of 2^96 stays far inside
+// fp32 (1e34 < 3.4e38, and O = sum P v below it for |v| up to 3e4), bf16 P has the fp32 exponent range.
+constexpr float kTop = 96.f;        // zero / fixed shift: largest exponent a term may reach
+constexpr float kMaxBound = 98.f;   // fixed shift: largest score bound b (smallest row-max term 2^(96 - 2 b) >= 2^-100)
+constexpr float kTopF8 = 60.f;      // fp8 Q K^T form: P = exp2(S) unshifted for bound products up to this
+constexpr float kLazy = 24.f;       // online max: rescale only when a row max exceeds the shift by more (P <= 2^24)
+
+typedef __attribute__((address_space(3))) const char* lds_char_ptr;
+
+// compile-time loop: f(integral_constant<int, I>) for I = 0 .. N-1, in order
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
+}
+
+// The lane index computed afresh where it is used (opaque to CSE / loop-invariant hoisting): the persistent form
+// recomputes its lane-dependent addresses per use instead of holding them in VGPRs across the tile loop, where a
+// 256-VGPR kernel would spill them and reload them behind a vmcnt(0) that drains the tile loads in flight.
+__device__ __forceinline__ int lane_fresh() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
+__device__ __forceinline__ float wave_swap_sum(float x) {  // lanes l and l ^ 32
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float group4_sum(float x) {  // over the 4 lane groups of 16 (lanes c, c+16, c+32, c+48)
+  x += __shfl_xor(x, 16);
+  return x + __shfl_xor(x, 32);
+}
+__device__ __forceinline__ float group4_max(float x) {  // the same reduction by row swaps (no LDS crossbar)
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1]));
+}
+
+struct AttnArgs {
+  const unsigned short* q; const unsigned short* k; const unsigned short* v; unsigned short* o;
+  int64_t q_sb, q_sl, q_sh;
+  int64_t k_sb, k_sl, k_sh;
+  int64_t v_sb, v_sl, v_sh;
+  int64_t o_sb, o_sl, o_sh;
+  int B, H, Lq, Lk;
+  int nqb;          // query blocks per (b, h)
+  int nsplit;       // key-range splits per (b, h, query block) (1: O written directly)
+  int tps;          // key tiles per split
+  int ntk_v;        // fp8 P.V: key tiles per (b, h) of the v8t layout (ceil(Lk / 64))
+  const float* v_amax;  // fp8 P.V: per-(b, h) max |v| (v8t holds v * 448 / amax)
+  float s_init;     // fp8 forms: the Q K^T chains' initial C (-shift: P = exp2(S - shift) stays inside e5m2)
+  float* o_part;    // nsplit > 1: [nsplit][B][H][Lq][128] fp32 partial O (normalised per split)
+  float* lse_part;  // nsplit > 1: [nsplit][B][H][Lq] fp32 log2-sum-exp2 of the scaled scores
+  float scale_log2; // softmax scale * log2(e) (1 for a pre-scaled q)
+  float kbound;     // > 0: upper bound of |k| over all keys (fixed shift where it allows); 0: online max only
+  const float* kslots;  // gated pair: max |k| over all keys = the max of n_kslots floats kslots[32 i] (device memory)
+  int n_kslots;
+};
+
+// ------------------------------------------------------------------------------------------------
+// attn_fwd_m16. Fragments (lane l, g = l >> 4, c = l & 15), per wave and 64-key tile:
+//   S^T = K Q^T: 4 key blocks kb x 2 query halves qh x 4 d-steps s = 32 MFMAs. A = K[16 kb + c][32 s + 8 g ..]
+//     (one ds_read_b128, shared by both qh), B = Q[16 qh + c][32 s + 8 g ..] (32 VGPRs resident), C: lane holds
+//     keys 16 kb + 4 g + i (i < 4) of query 16 qh + c: every lane owns two query rows and 16 keys of each.
+//   O^T = V^T P^T: 8 d blocks db x 2 qh x 2 key steps ks = 32 MFMAs. B = P^T packed lane-locally from the two S
+//     blocks kb = 2 ks, 2 ks + 1 (k slot 8 g + j <-> key 32 ks + 16 (j >> 2) + 4 g + (j & 3)); A = V^T in that
+//     same key order: two ds_read_b64_tr_b16 (rows 32 ks + 4 g + q and 32 ks + 16 + 4 g + q, columns 16 db + 4 p
+//     for lane 16 g + 4 q + p), shared by both qh.
+//   Row sums: one MFMA per key step and qh multiplies P^T by an all-ones V^T row (4 per tile): the sum of the bf16
+//     P the P.V MFMAs used, complete in every lane.
+// LDS rows of 288 B (256 + 32) for K and V: the ds_read_b128 K fragment read lands on 16-B slot (2 c + g + 4 s) mod
+// 16, distinct within every lane group the LDS services together (MI355X_MICROARCH §LDS); the transposed V reads
+// land on 8 distinct 32-B bank groups. SQ_LDS_BANK_CONFLICT = 0 measured.
+//
+// Ping-pong: waves w and w + 4 share a SIMD; group A (waves 0-3) and group B (waves 4-7) run opposite phases:
+//   phase 2t  : A  MFMA  P.V(t), S(t+1) = K(t+1) Q^T     B  softmax S(t) -> P(t), stage K(t+2)
+//   phase 2t+1: A  softmax S(t+1) -> P(t+1), stage V(t+1) B  MFMA (same products as A's)
+// The MFMA phase's wave runs at s_setprio 1; its operand reads are inline asm issued 3 pairs ahead into a 4-deep
+// ring, each pair behind a counted lgkmcnt naming its operand; group B issues its first 3 pairs at the end of its
+// softmax phase (its V(t) and K(t+1) were written at least one barrier earlier). P.V(t) runs before Q K^T(t+1), so
+// P^T (16 VGPRs) is dead before S^T (32) is written and the two share registers.
+//
+// Softmax shift (per query row, log2 units). Softmax is shift invariant; the shift only has to keep every term in
+// the fp32 / bf16 range. With a pre-scaled q (rows carry softmax_scale * log2 e) the shift is the initial C of the
+// row's Q K^T chains, so S arrives already shifted:
+//   zero   (pre-scaled q, bound product b <= 96): no shift; terms in [2^-b, 2^b];
+//   fixed  (b <= 98): shift max(b_row - 96, 0) from the row's own |q_row|; the row's largest term >= 2^-100;
+//   online (larger or unknown bounds): tile 0 sets the shift to the row max; a later tile rescales O and the row sum
+//          (and moves the shift) only for a row whose max exceeds the shift by more than kLazy (24), so P <= 2^24 and
+//          the row's largest term >= 1. Per tile: 16 v_max3 per lane and one ballot; the row reduction (two row swaps)
+//          and the rescale run only when a lane's own tile max crosses the threshold (rare after tile 0; rows below it
+//          take the branch with d = 0, exactly, so rows stay independent of each other).
+// The host picks the mode from the bounds (m16_mode).
+constexpr int kKStride16 = 288;
+constexpr int kVStride16 = 288;
+// MFMA phase: operand pairs read ahead of their MFMAs. 2 (ring of 3 fragments) frees 4 VGPRs against 3: the online
+// form -3.4 % per launch, zero shift -0.1 %, 4: online +7 % (profiles/r3/attn_nop/ring_depth_ab.log, ring_depth2_ab.log)
+constexpr int kAhead = 2;
+constexpr int kKBuf16 = kKBlk * kKStride16;        // 18432
+constexpr int kVBuf16 = kKBlk * kVStride16;        // 18432
+constexpr int kLds16 = 2 * kKBuf16 + 2 * kVBuf16;  // 73728
+
+// Persistent short-key form (kPersist, text cross-attention): one workgroup per CU walks a contiguous run of
+// (b, h, query block) blocks as ONE stream of key tiles (tile t = key tile t mod ntk of the run's block t / ntk), so
+// the K/V pipeline never drains between blocks and a block's prologue (its Q) and epilogue (its O stores) hide
+// under the neighbouring tiles' work:
+//   * each wave copies its next block's Q fragments (8 KiB, in its own ds_read_b128 lane order) into a private LDS
+//     slot by LDS-DMA in the softmax phase of one of the block's tiles 0 .. ntk - 2 (kQCopyStagger), and reads them into its Q
+//     registers in the softmax phase of the block's last tile (after the last Q K^T of the old block, before the
+//     first of the new);
+//   * the softmax phase that opens a block first normalises the finished block's O into the same slot as row-major
+//     bf16 rows and stores them from there as whole 256-B rows (four rows per store instruction instead of 16-B
+//     pieces of 16 rows at the token stride), then zeroes O. Isolation probes (lab builds without the copy / without the
+//     stores, profiles/r3/xattn_persistent/boundary_probe_v*.log): the copy's exposed HBM latency and the stores are
+//     what remains of the block seam.
+// Each block's arithmetic is the per-block kernel's, operation for operation (the online shift restarts from 0),
+// so the two forms are bit-identical. Needs ntk >= 2 (the last Q piece lands at least one phase pair before its read).
+// The next block's Q copy is issued whole (8 KiB per wave) in one softmax phase, at a tile that differs between
+// workgroups (kQCopyStagger). Issued at tile 0 in every workgroup it was a chip-wide burst of 256 x 64 KiB at once whose
+// HBM latency the staging wait two phases later (in-order vmcnt) waited out: -10 % without the copy
+// (boundary_probe_v1.log). Spread one piece per tile it measured slower still (every tile then waits on a piece,
+// boundary_probe_v2.log).
+constexpr bool kQCopyStagger = true;
+constexpr int kOStr = 272;                          // staged O row stride (256 B + 16: conflict-free b64 writes)
+constexpr int kQSlot = kQRows * kOStr;              // per wave 8704 B: next-block Q fragments (8 KiB) / staged O rows
+constexpr int kLdsP = kLds16 + kWaves * kQSlot;     // 143360
+
+// kMode: 0 fixed shift, 1 fixed shift known to be 0 (pre-scaled q, bound product <= 96: no initial C), 2 online.
+// kGate (cp25_attn_fwd_prescaled_kslots: a data-tight key bound in device memory, the max |k| the producing RMSNorm
+// kernel measured): the same grid is launched twice, kGate 1 with kMode 1 and kGate 2 with kMode 2; a workgroup
+// whose query block's bound max|q_row| max|k| is <= 96 runs in the first launch (no shift, the fast loop) and exits
+// at once in the second, any other runs in the second (online max). Each block's arithmetic is exactly that of its
+// mode; which mode a row gets depends on the other rows of its 256-row block.
+template <int kKind, bool kPre, int kMode, bool kPersist = false, int kGate = 0>
+__global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[kPersist ? kLdsP : kLds16];
+  constexpr int KB1 = kKBuf16, VB0 = 2 * kKBuf16;
+  static_assert(kMode >= 0 && kMode <= 2 && (kMode != 1 || kPre), "kMode: 0 fixed, 1 zero shift, 2 online");
+  static_assert(!kPersist || (kKind == 1 && kMode != 0), "persistent form: cross-attention, zero shift or online");
+  constexpr bool online = kMode == 2;
+  constexpr bool kInit = kPre && kMode != 1;  // the shift rides in the Q K^T chains' initial C
+
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  // persistent: this workgroup's run [blk0, blk_end) of blocks bh * nqb + qb (an XCD's workgroups hold one
+  // contiguous range, so they stream the K/V of a few (b, h) through its L2)
+  int blk0 = 0, blk_end = 0;
+  if constexpr (kPersist) {
+    const int64_t nb = (int64_t)a.B * a.H * a.nqb;
+    blk0 = (int)(tile * nb / gridDim.x);
+    blk_end = (int)((tile + 1) * nb / gridDim.x);
+  }
+  // tile order (b, h) > split > query block: an XCD's contiguous tile range streams one key range
+  const int qb = (kPersist ? blk0 : tile) % a.nqb;
+  const int bhs = (kPersist ? blk0 : tile) / a.nqb;
+  const int split = bhs % a.nsplit, bh = bhs / a.nsplit;
+  const int b = bh / a.H, h = bh % a.H;
+  const int key0 = split * a.tps * kKBlk;
+  const int Lk = min(a.Lk - key0, a.tps * kKBlk);  // this workgroup's keys as a self-contained sequence
+  const int ntk = (Lk + kKBlk - 1) / kKBlk;         // key tiles per block
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int c16 = lane & 15;
+  const int g = lane >> 4;
+  const bool group_b = __builtin_amdgcn_readfirstlane(tid) >= kThreads / 2;
+  const int wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);  // the wave index as a scalar (persistent form)
+
+  const unsigned short* qp = a.q + b * a.q_sb + h * a.q_sh;
+  const unsigned short* kp = a.k + b * a.k_sb + h * a.k_sh + (int64_t)key0 * a.k_sl;
+  const unsigned short* vp = a.v + b * a.v_sb + h * a.v_sh + (int64_t)key0 * a.v_sl;
+
+  // ---- Q fragments (B operand): Q[16 qh + c][32 s + 8 g .. +7] ----
+  int q_row[2];
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int qh = 0; qh < 2; ++qh) {
+    q_row[qh] = qb * kQBlk + wave * kQRows + 16 * qh + c16;
+    const unsigned short* src = qp + (int64_t)min(q_row[qh], a.Lq - 1) * a.q_sl + 8 * g;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[qh][s] = *reinterpret_cast<const bf16x8*>(src + 32 * s);
+  }
+
+  if constexpr (kGate != 0) {
+    static_assert(kPre && !kPersist && ((kGate == 1 && kMode == 1) || (kGate == 2 && kMode == 2)), "gated pair");
+    __shared__ float gate_max[kWaves];
+    float km = lane < a.n_kslots ? a.kslots[32 * lane] : 0.f;  // max |k| over all keys (slots 128 B apart)
+    float qm = 0.f;                                      // max |q_row| over this wave's rows
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      float qq = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = static_cast<float>(qf[qh][s][e]);
+          qq = fmaf(x, x, qq);
+        }
+      qm = fmaxf(qm, sqrtf(group4_sum(qq)));
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      km = fmaxf(km, __shfl_xor(km, m));
+      qm = fmaxf(qm, __shfl_xor(qm, m));
+    }
+    if (lane == 0) gate_max[wave] = qm;
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) qm = fmaxf(qm, gate_max[w]);
+    // bound product with a 1e-3 margin (fp32 sums of the scores and of the norms); no slots written: online
+    const bool zero_ok = km > 0.f && qm * km * 1.001f <= kTop;
+    if (zero_ok != (kGate == 1)) return;  // uniform over the workgroup
+  }
+
+  f32x4 o[8][2];
+#pragma unroll
+  for (int d = 0; d < 8; ++d)
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) o[d][qh] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 lsum[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  typedef short s16x8v __attribute__((ext_vector_type(8)));
+  const bf16x8 ones8 = __builtin_bit_cast(bf16x8, s16x8v{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80});
+
+  // ---- the rows' softmax shifts: fixed from |q_row| and the key bound (the host checked b_row <= 98), or online ----
+  const float cs = kPre ? 1.f : a.scale_log2;  // score -> log2 units
+  float m_run[2] = {0.f, 0.f};
+  if constexpr (kMode == 0) {
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      float qq = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = static_cast<float>(qf[qh][s][e]);
+          qq = fmaf(x, x, qq);
+        }
+      m_run[qh] = fmaxf(sqrtf(group4_sum(qq)) * a.kbound * cs - kTop, 0.f);
+    }
+  }
+  f32x4 minit[2];  // kPre: -shift, the Q K^T chains' initial C
+#pragma unroll
+  for (int qh = 0; qh < 2; ++qh) minit[qh] = f32x4{-m_run[qh], -m_run[qh], -m_run[qh], -m_run[qh]};
+
+  const int ntiles = kPersist ? (blk_end - blk0) * ntk : ntk;
+  const int copy_tile = kPersist && ntk > 1 ? (kQCopyStagger ? (int)(blockIdx.x % (unsigned)(ntk - 1)) : 0) : 0;
+
+  // staging: a group's 256 threads own rows u/16 + 16 i, chunk u%16 of a 64 x 128 tile. buffer_load with a
+  // wave-uniform descriptor (SALU-only addressing); rows past Lk fall outside its range and read as zero (their
+  // scores are masked to -inf)
+  const int u = tid & (kThreads / 2 - 1);
+  const int srow = u >> 4, sch = u & 15;
+  const int64_t sl = group_b ? a.k_sl : a.v_sl;
+  const char* sbase = group_b ? (const char*)kp : (const char*)vp;
+  const int st_off = (int)(srow * sl * 2) + sch * 16, st_step = (int)(16 * sl * 2);
+  u32x4 st[4];
+  auto load_tile = [&](int t) __attribute__((always_inline)) {
+    const char* base;
+    int kt;
+    if constexpr (kPersist) {  // key tile kt of block blk0 + t / ntk (wave-uniform scalar arithmetic)
+      const int tb = t / ntk;
+      kt = t - tb * ntk;
+      const int bh_t = (blk0 + tb) / a.nqb;
+      const int b_t = bh_t / a.H, h_t = bh_t % a.H;
+      base = group_b ? (const char*)(a.k + b_t * a.k_sb + h_t * a.k_sh) : (const char*)(a.v + b_t * a.v_sb + h_t * a.v_sh);
+    } else {
+      kt = t;
+      base = sbase;
+    }
+    const int rows = (kPersist && t >= ntiles) ? 0 : min(Lk - kt * kKBlk, kKBlk);  // past the run: no bytes
+    const int nbytes = rows > 0 ? (int)((rows - 1) * sl * 2) + 2 * kD : 0;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(base + (int64_t)kt * kKBlk * sl * 2), (short)0, nbytes,
+                                                        0x00020000);
+    int off = st_off;
+    if constexpr (kPersist) {  // u = 64 (wave & 3) + lane: row u / 16, 16-B chunk u % 16
+      const int uf = ((wave_u & 3) << 6) + lane_fresh();
+      off = (uf >> 4) * (int)(sl * 2) + (uf & 15) * 16;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      st[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + i * st_step, 0, 0));
+  };
+  char* const k_wr = smem + srow * kKStride16 + sch * 16;
+  char* const v_wr = smem + VB0 + srow * kVStride16 + sch * 16;
+  auto write_k = [&](auto BUF) __attribute__((always_inline)) {
+    constexpr int kb = decltype(BUF)::value ? KB1 : 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(k_wr + kb + 16 * i * kKStride16) = st[i];
+  };
+  auto write_v = [&](auto BUF) __attribute__((always_inline)) {
+    constexpr int vb = decltype(BUF)::value ? kVBuf16 : 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(v_wr + vb + 16 * i * kVStride16) = st[i];
+  };
+
+  // per-lane LDS read bases; everything else is an immediate offset
+  const char* const k_rd = smem + c16 * kKStride16 + 16 * g;                                    // + KB + 16 kb rows + 64 s
+  const char* const v_rd = smem + VB0 + (4 * g + (c16 >> 2)) * kVStride16 + 8 * (c16 & 3);      // + VB + rows + 32 db
+  const unsigned k_rd_lds = (unsigned)(uintptr_t)(lds_char_ptr)k_rd;
+  const unsigned v_rd_lds = (unsigned)(uintptr_t)(lds_char_ptr)v_rd;
+
+  const int ragged_tile = (Lk % kKBlk) != 0 ? Lk / kKBlk : -1;
+
+  f32x4 S[4][2];   // S^T of the tile awaiting its softmax: [key block][query half]
+  bf16x8 pb[2][2]; // P^T of the tile awaiting its P.V: [key step][query half]
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+
+  // O rows of query half qh (lane holds O^T[16 db + 4 g + i][16 qh + c]) normalised by inv and stored to op (the
+  // row's d = 0): the text cross-attention's 16-B form (8 key tiles per block, so the store tail counts): 8 x 16 B
+  // per lane instead of 16 x 8 B (the tail is store-issue-bound, cdna_hip_programming T21; 1.278 -> 1.228 ms per
+  // launch, same box, profiles/r3/attn_epilogue_ab.log). For each pair of d blocks (2m, 2m + 1) the lane rows g and
+  // g ^ 1 (lanes l, l ^ 16) swap halves with one v_permlane16_swap per dword (odd rows of the first operand <-> even
+  // rows of the second), so an even-g lane holds d 32 m + 4 g .. + 8 of block 2m and an odd-g lane d 32 m + 16 +
+  // 4 (g - 1) .. + 8 of block 2m + 1.
+  auto store_rows16 = [&](unsigned short* row_d0, int qh, float inv, int gl) __attribute__((always_inline)) {
+    const bool odd = gl & 1;
+    unsigned short* op = row_d0 + (odd ? 16 + 4 * (gl - 1) : 4 * gl);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      unsigned lo[2], hi[2];  // block 2m, block 2m + 1 (two packed bf16 pairs each)
+#pragma unroll
+      for (int w = 0; w < 2; ++w) {
+        lo[w] = f2bf(o[2 * m][qh][2 * w] * inv) | ((unsigned)f2bf(o[2 * m][qh][2 * w + 1] * inv) << 16);
+        hi[w] = f2bf(o[2 * m + 1][qh][2 * w] * inv) | ((unsigned)f2bf(o[2 * m + 1][qh][2 * w + 1] * inv) << 16);
+        const auto r = __builtin_amdgcn_permlane16_swap(lo[w], hi[w], false, false);
+        lo[w] = r[0];
+        hi[w] = r[1];
+      }
+      *reinterpret_cast<u32x4*>(op + 32 * m) = u32x4{lo[0], lo[1], hi[0], hi[1]};
+    }
+  };
+
+  // ---- persistent form: block bookkeeping (all wave-uniform scalar work) ----
+  auto block_rows = [&](int blk, const unsigned short*& base, int& row0, int64_t sb, int64_t sh,
+                        const unsigned short* p) __attribute__((always_inline)) {
+    const int bh_n = blk / a.nqb;
+    row0 = (blk - bh_n * a.nqb) * kQBlk + wave_u * kQRows;
+    base = p + (bh_n / a.H) * sb + (bh_n % a.H) * sh;
+  };
+  // copy block blk's Q fragments of this wave into its LDS slot: lane l's 16 B of (qh, s) land at 1 KiB (qh, s) + 16 l,
+  // exactly where its ds_read_b128 reads them back
+  // pieces [p_lo, p_hi) of the copy (piece p = (qh, s) = (p / 4, p % 4))
+  auto dma_q = [&](int blk, int p_lo, int p_hi) __attribute__((always_inline)) {
+    const unsigned short* base;
+    int row0;
+    block_rows(blk, base, row0, a.q_sb, a.q_sh, a.q);
+    const int lf = lane_fresh();
+    char* const q_slot = smem + kLds16 + wave_u * kQSlot;  // this wave's slot
+    for (int p = p_lo; p < p_hi; ++p) {
+      const int qh = p >> 2, s = p & 3;
+      const unsigned short* src =
+          base + (int64_t)min(row0 + 16 * qh + (lf & 15), a.Lq - 1) * a.q_sl + 8 * (lf >> 4) + 32 * s;
+      // inline asm, not the builtin: with a compiler-visible LDS-DMA in the loop the compiler drains vmcnt before
+      // every s_barrier (the tile loads in flight included). Hidden from its waitcnt model, the copy is only ever
+      // over-waited for (its counts are then too small); the read in softmax() waits for it explicitly. M0 is a
+      // reserved register the compiler does not allocate; nothing else in this kernel uses it (checked in the ISA).
+      const unsigned dst = (unsigned)(uintptr_t)(lds_char_ptr)(q_slot + p * 1024);
+      asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(dst) : "memory");
+    }
+  };
+  // normalise the finished block's O into this wave's slot as row-major bf16 rows, store them as whole rows, zero O
+  // (nsplit == 1). The slot is free: this block's Q was read from it a phase pair ago, the next copy starts after.
+  auto store_block = [&](int blk) __attribute__((always_inline)) {
+    const unsigned short* base;
+    int row0;
+    block_rows(blk, base, row0, a.o_sb, a.o_sh, a.o);
+    const int lf = lane_fresh();
+    char* const slot = smem + kLds16 + wave_u * kQSlot;
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      const float inv = 1.f / lsum[qh][0];
+      char* const wr = slot + (16 * qh + (lf & 15)) * kOStr + 8 * (lf >> 4);  // row 16 qh + c, d = 16 db + 4 g
+#pragma unroll
+      for (int db = 0; db < 8; ++db) {
+        u16x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = f2bf(o[db][qh][e] * inv);
+        *reinterpret_cast<u16x4*>(wr + 32 * db) = w;
+      }
+      lsum[qh] = zero4;
+#pragma unroll
+      for (int db = 0; db < 8; ++db) o[db][qh] = zero4;
+    }
+    // store i: rows 4 i .. 4 i + 3 of the wave's 32, lane l row 4 i + l / 16, 16-B chunk l % 16 (one wave's LDS
+    // writes and reads execute in order)
+    const char* const rd = slot + (lf >> 4) * kOStr + 16 * (lf & 15);
+    unsigned short* const wo = const_cast<unsigned short*>(base) + 8 * (lf & 15);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = 4 * i + (lf >> 4);
+      const u32x4 v = *reinterpret_cast<const u32x4*>(rd + 4 * i * kOStr);
+      if (row0 + r < a.Lq) *reinterpret_cast<u32x4*>(wo + (int64_t)(row0 + r) * a.o_sl) = v;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read back before the next Q copy lands in the slot
+  };
+
+  auto qk_mma = [&](auto BUF) __attribute__((always_inline)) {
+    constexpr int kb = decltype(BUF)::value ? KB1 : 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(k_rd + kb + k4 * 16 * kKStride16 + 64 * s);
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh)
+          S[k4][qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qh][s], s == 0 ? (kInit ? minit[qh] : zero4) : S[k4][qh],
+                                                              0, 0, 0);
+      }
+  };
+  auto softmax = [&](int t_run) __attribute__((always_inline)) {
+    // persistent: key tile t of block blk0 + tb; a block's first tile opens with the previous block's O stores and
+    // this block's next-block Q copy
+    int t = t_run, tb = 0;
+    if constexpr (kPersist) {
+      tb = t_run / ntk;
+      t = t_run - tb * ntk;
+      if (t == 0 && tb > 0) store_block(blk0 + tb - 1);
+      // the next block's Q copy, whole, in the softmax phase of tile (workgroup mod (ntk - 1)): the workgroups' block
+      // seams run in lock step, so a copy at tile 0 everywhere was one chip-wide HBM burst per block
+      if (t == copy_tile && blk0 + tb + 1 < blk_end) dma_q(blk0 + tb + 1, 0, 8);
+    }
+    if (__builtin_expect(t == ragged_tile, 0)) {
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = t * kKBlk + 16 * k4 + 4 * g + i;
+          if (key >= Lk) {
+            S[k4][0][i] = -INFINITY;
+            S[k4][1][i] = -INFINITY;
+          }
+        }
+    }
+    // S enters here: keeps the (otherwise dependency-free) exp work from being hoisted across the barrier into the
+    // MFMA phase
+    asm volatile("" : "+v"(S[0][0]), "+v"(S[0][1]), "+v"(S[1][0]), "+v"(S[1][1]), "+v"(S[2][0]), "+v"(S[2][1]),
+                 "+v"(S[3][0]), "+v"(S[3][1]));
+    if constexpr (online) {
+      float mx[2];  // this lane's part of each row's tile max, above the row's current shift
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) {
+        float x = fmaxf(S[0][qh][0], S[0][qh][1]);
+#pragma unroll
+        for (int i = 2; i < 16; i += 2) x = fmaxf(fmaxf(x, S[i >> 2][qh][i & 3]), S[(i + 1) >> 2][qh][(i + 1) & 3]);
+        mx[qh] = kPre ? x : fmaf(x, cs, -m_run[qh]);
+      }
+      if (__builtin_expect(t == 0 || __any(fmaxf(mx[0], mx[1]) > kLazy), 0)) {
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) mx[qh] = group4_max(mx[qh]);  // the whole row's (the shift is per row)
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) {
+          // tile 0: the shift becomes the row max (O and the sum are still zero); later: only a row past the lazy
+          // threshold moves (d = 0 elsewhere: x 1 and - 0 are exact), so a row's result never depends on the other
+          // rows of its wave (CP shards and key splits that regroup rows into waves stay bit-identical)
+          const float d = t == 0 ? mx[qh] : (mx[qh] > kLazy ? mx[qh] : 0.f);
+          const float alpha = t == 0 ? 0.f : __builtin_amdgcn_exp2f(-d);
+          m_run[qh] += d;
+          lsum[qh] *= alpha;
+#pragma unroll
+          for (int db = 0; db < 8; ++db) o[db][qh] *= alpha;
+          if constexpr (kPre) {
+#pragma unroll
+            for (int k4 = 0; k4 < 4; ++k4) S[k4][qh] -= d;
+            minit[qh] = f32x4{-m_run[qh], -m_run[qh], -m_run[qh], -m_run[qh]};
+          }
+        }
+      }
+    } else {
+      // contract guard: a norm bound below the real norms can only show as an overflowed row sum (moderate
+      // violations are exact by shift invariance); poison the rows (NaN) instead of returning wrong ones
+      if (__builtin_expect(__any(fmaxf(lsum[0][0], lsum[1][0]) > 3.0e38f), 0)) {
+        const float nan = __uint_as_float(0x7fc00000u);
+#pragma unroll
+        for (int d = 0; d < 8; ++d) o[d][0] = o[d][1] = f32x4{nan, nan, nan, nan};
+      }
+    }
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float sv = S[2 * ks + (j >> 2)][qh][j & 3];
+          v[j] = static_cast<__bf16>(__builtin_amdgcn_exp2f(kPre ? sv : fmaf(sv, cs, -m_run[qh])));
+        }
+        pb[ks][qh] = v;
+      }
+    // keep the whole softmax in this phase: s_barrier orders memory only
+    asm volatile("" ::"v"(pb[0][0]), "v"(pb[0][1]), "v"(pb[1][0]), "v"(pb[1][1]));
+    if constexpr (kPersist) {
+      // the block's last tile: its Q K^T is done, the next MFMA phase computes the next block's first Q K^T, which
+      // starts from the per-block kernel's state (next block's Q, shift 0)
+      if (t == ntk - 1 && blk0 + tb + 1 < blk_end) {
+        const char* qsrc = smem + kLds16 + wave_u * kQSlot + 16 * lane_fresh();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's Q copy (issued >= 1 phase pair ago) landed
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) qf[qh][s] = *reinterpret_cast<const bf16x8*>(qsrc + (qh * 4 + s) * 1024);
+        if constexpr (online) {
+#pragma unroll
+          for (int qh = 0; qh < 2; ++qh) {
+            m_run[qh] = 0.f;
+            minit[qh] = f32x4{-0.f, -0.f, -0.f, -0.f};
+          }
+        }
+      }
+    }
+  };
+
+  typedef std::integral_constant<int, 0> B0;
+  typedef std::integral_constant<int, 1> B1;
+
+  // ---- prologue: K(0), V(0) -> buffer 0; K(1) -> buffer 1; S(0) for everyone, P(0) for A ----
+  load_tile(0);
+  if (group_b) write_k(B0{}); else write_v(B0{});
+  if (group_b) {
+    load_tile(1);
+    write_k(B1{});
+    load_tile(2);  // written in phase 0
+  } else {
+    load_tile(1);  // written in phase 1
+  }
+  __syncthreads();
+  qk_mma(B0{});
+  if (!group_b) softmax(0);
+  // (group A's phase-closing barrier follows the pre-issue of its first MFMA phase's reads, below)
+  if (group_b) __syncthreads();
+
+  // one MFMA phase: the 4 row-sum MFMAs, P.V of tile t, then Q K^T of tile t+1 (64 MFMAs of 16 cycles). Operand pair
+  // n (one fragment, two MFMAs, one per query half): n < 16 the V^T fragment (db = n & 7, ks = n >> 3, two
+  // transposed reads), n >= 16 the K fragment (kb = (n - 16) & 3, s = (n - 16) >> 2). (The Q K^T after the last tile
+  // reads a stale K buffer; its scores are never used.) A phase issues its pairs in the order of slot s = 0 .. 31,
+  // pair (s + rot) mod 32: group B P.V first (rot 0), group A Q K^T first (rot 16), so that A, too, can issue its
+  // first pairs before the barrier that opens the phase (K(t+1) was written two phases earlier; V(t) is A's own
+  // staging of the phase just ending, readable only after that barrier).
+  constexpr int kR = kAhead + 1;
+  bf16x8 ring[kR];
+  constexpr auto rot_pair = [](int s_, int rot) constexpr { return s_ < 32 ? (s_ + rot) & 31 : s_; };
+  constexpr auto nreads = [](int n) constexpr { return n >= 32 ? 0 : (n >= 16 ? 1 : 2); };
+  typedef std::integral_constant<int, 0> R0;
+  typedef std::integral_constant<int, 16> R16;
+  auto issue_pair = [&](auto PAR, auto SC, auto ROT) __attribute__((always_inline)) {
+    constexpr int par = decltype(PAR)::value;
+    constexpr int kbuf = (par ^ 1) ? KB1 : 0;  // K(t+1)
+    constexpr int vbuf = par ? kVBuf16 : 0;    // V(t), relative to VB0
+    constexpr int slot = decltype(SC)::value;
+    constexpr int n = rot_pair(slot, decltype(ROT)::value);
+    if constexpr (n >= 16 && n < 32) {
+      constexpr int m = n - 16;
+      constexpr int off = kbuf + (m & 3) * 16 * kKStride16 + 64 * (m >> 2);
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ring[slot % kR]) : "v"(k_rd_lds), "i"(off));
+    } else if constexpr (n < 16) {
+      constexpr int off = vbuf + 32 * (n >> 3) * kVStride16 + 32 * (n & 7);
+      s16x4 lo, hi;
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(v_rd_lds), "i"(off));
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(v_rd_lds), "i"(off + 16 * kVStride16));
+      typedef short s16x8 __attribute__((ext_vector_type(8)));
+      const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      ring[slot % kR] = __builtin_bit_cast(bf16x8, r);
+    }
+  };
+  // the phase's first kAhead pairs, issued before the barrier that opens it, and the LDS reads they leave in flight
+  auto pre_issue = [&](auto PAR, auto ROT) __attribute__((always_inline)) {
+    static_for<kAhead>([&](auto SC) __attribute__((always_inline)) { issue_pair(PAR, SC, ROT); });
+  };
+  constexpr auto pre_reads = [=](int rot) constexpr {
+    int p = 0;
+    for (int i = 0; i < kAhead; ++i) p += nreads(rot_pair(i, rot));
+    return p;
+  };
+  // PRE: the first kAhead pairs were issued before the barrier that opens the phase (pre_issue)
+  auto mfma_phase = [&](auto PAR, auto PRE, auto ROT) __attribute__((always_inline)) {
+    constexpr int rot = decltype(ROT)::value;
+    auto issue = [&](auto SC) __attribute__((always_inline)) { issue_pair(PAR, SC, ROT); };
+    __builtin_amdgcn_s_setprio(1);
+    // the first kAhead pairs are in flight (PRE): the loop's counted waits retire them
+    if constexpr (!decltype(PRE)::value) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      static_for<kAhead>(issue);
+    }
+    // row sums of P(t) first: they need no LDS operand, so they cover the first operand reads' latency (after the
+    // P.V pairs they measured 0.25 % slower, profiles/r3/attn_nop/barrier_rowsum_ab.log)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) lsum[qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones8, pb[ks][qh], lsum[qh], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<32>([&](auto NC) __attribute__((always_inline)) {
+      constexpr int n = decltype(NC)::value;
+      issue(std::integral_constant<int, n + kAhead>{});
+      constexpr int pending = [=]() constexpr {
+        int p = 0;
+        for (int i = 1; i <= kAhead; ++i) p += nreads(rot_pair(n + i, rot));
+        return p;
+      }();
+      constexpr int pn = rot_pair(n, rot);  // this slot's pair
+      // The wait READS the operand ("v" input) and a scheduling barrier keeps the MFMAs behind it. An input keeps the
+      // asynchronously written register allocated until its data has landed (also when the MFMAs that use it are
+      // dead, as in the Q K^T after the last tile); the previous form, an asm "redefining" it ("+v"), made the hazard
+      // recognizer treat it as a VALU write and pad every MFMA pair with an s_nop (-2.3 % per launch without them,
+      // profiles/r3/attn_nop/self_nop_ab.log).
+      asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(pending), "v"(ring[n % kR]) : "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) {
+        if constexpr (pn >= 16) {
+          constexpr int m = pn - 16;
+          S[m & 3][qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              ring[n % kR], qf[qh][m >> 2], m < 4 ? (kInit ? minit[qh] : zero4) : S[m & 3][qh], 0, 0, 0);
+        } else {
+          o[pn & 7][qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[n % kR], pb[pn >> 3][qh], o[pn & 7][qh], 0, 0, 0);
+        }
+      }
+      // program order = issue order (the scheduler otherwise sinks MFMAs below later reads and renames accumulators)
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // a raw barrier behind a counted wait: the phase's LDS writes retire, the pre-issued reads stay in flight across it
+  // (a __syncthreads() fence waited for them too, before the barrier, on the longer phase)
+  auto barrier_pre = [&](auto ROT) __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(pre_reads(decltype(ROT)::value)) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  if (!group_b) {
+    // group A: phase 2t MFMA (Q K^T(t+1) first), phase 2t+1 softmax(t+1) + V(t+1) staging + the next phase's first
+    // K reads
+    pre_issue(B0{}, R16{});
+    barrier_pre(R16{});
+    auto step = [&](auto PAR, int t) __attribute__((always_inline)) {
+      constexpr int par = decltype(PAR)::value;
+      mfma_phase(PAR, std::true_type{}, R16{});
+      __syncthreads();
+      if (t + 1 < ntiles) {
+        write_v(std::integral_constant<int, par ^ 1>{});  // drains under the softmax VALU
+        softmax(t + 1);
+        load_tile(t + 2);
+        pre_issue(std::integral_constant<int, par ^ 1>{}, R16{});
+        barrier_pre(R16{});
+      } else {
+        __syncthreads();
+      }
+    };
+    // pairs of tiles (constexpr buffer parity), then the odd last tile: one loop exit
+    for (int t = 0; t + 1 < ntiles; t += 2) {
+      step(B0{}, t);
+      step(B1{}, t + 1);
+    }
+    if (ntiles & 1) step(B0{}, ntiles - 1);
+  } else {
+    // group B: phase 2t softmax(t) + K(t+2) staging, phase 2t+1 MFMA
+    auto step = [&](auto PAR, int t) __attribute__((always_inline)) {
+      if (t + 2 < ntiles) write_k(PAR);
+      softmax(t);
+      if (t + 2 < ntiles) load_tile(t + 3);
+      pre_issue(PAR, R0{});
+      barrier_pre(R0{});  // the K(t+2) writes retire
+      mfma_phase(PAR, std::true_type{}, R0{});
+      __syncthreads();
+    };
+    for (int t = 0; t + 1 < ntiles; t += 2) {
+      step(B0{}, t);
+      step(B1{}, t + 1);
+    }
+    if (ntiles & 1) step(B0{}, ntiles - 1);
+  }
+
+  // ---- epilogue: lane holds O^T[16 db + 4 g + i][16 qh + c]: row q_row[qh], d = 16 db + 4 g + (0..3) ----
+  if constexpr (kPersist) {
+    store_block(blk_end - 1);
+    return;
+  }
+#pragma unroll
+  for (int qh = 0; qh < 2; ++qh) {
+    const float l_tot = lsum[qh][0];
+    const float inv = 1.f / l_tot;
+    if (q_row[qh] >= a.Lq) continue;
+    if (a.nsplit > 1) {
+      const int64_t row = ((int64_t)(split * a.B + b) * a.H + h) * a.Lq + q_row[qh];
+      float* op = a.o_part + row * kD + 4 * g;
+#pragma unroll
+      for (int db = 0; db < 8; ++db) {
+        f32x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = o[db][qh][e] * inv;
+        *reinterpret_cast<f32x4*>(op + 16 * db) = w;
+      }
+      if (g == 0) a.lse_part[row] = m_run[qh] + __log2f(l_tot);
+    } else if constexpr (kKind == 1) {
+      // cross-attention: the 16-B stores (the self-attention keeps the 8-B stores: with 1 705 key tiles per workgroup
+      // the tail is noise, and the 16-B form's register allocation measured 0.9 % slower there)
+      store_rows16(a.o + b * a.o_sb + h * a.o_sh + (int64_t)q_row[qh] * a.o_sl, qh, inv, g);
+    } else {
+      unsigned short* op = a.o + b * a.o_sb + h * a.o_sh + (int64_t)q_row[qh] * a.o_sl + 4 * g;
+#pragma unroll
+      for (int db = 0; db < 8; ++db) {
+        u16x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = f2bf(o[db][qh][e] * inv);
+        *reinterpret_cast<u16x4*>(op + 16 * db) = w;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// attn_fwd_f8: the config-5 fp8 option on v_mfma_f32_32x32x64_f8f6f4 (8 waves x 32 query rows per workgroup, swapped
+// products S^T = K Q^T and O^T = V^T P^T, the same ping-pong of the two waves of a SIMD as attn_fwd_m16).
+//   kF8 = 1 (cp25_attn_fwd_prescaled_fp8qk): q and k arrive as OCP e4m3 bytes (strides in bytes); Q K^T is 4 MFMAs of
+//     64 k per tile instead of 16 of 16, K tiles of 64 rows x 128 B (LDS rows 144 B). The operands' k order only has
+//     to agree between A and B: lane half h, byte i of both is d = 64 s + 32 h + i. P and V bf16 (V^T by
+//     ds_read_b64_tr_b16 from 320-B LDS rows), P = exp2(S) with no shift (host: |q| |k| <= kTopF8 = 60).
+//   kF8 = 3 (cp25_attn_fwd_prescaled_fp8): also O^T += V^T P^T on fp8: P^T as e5m2 bytes straight from the S^T
+//     accumulator (byte j = 16 kt + r) made without exp2 (n = round(4 (S - shift) + 60) clamped to [0, 255] by one
+//     v_cvt_pk_u8_f32 after one fma is read as e5m2, i.e. 2^(n / 4 - 15) with a linear mantissa), V^T as e4m3 from
+//     the v8t layout (cp25_cast_v_fp8t: per-(b, h) scale, keys permuted to the P bytes), 4 MFMAs per tile instead of
+//     16, LDS V rows of 64 B padded to 80; the row sums from a fifth MFMA against an all-ones V^T row (the sums of
+//     the P actually used). The shift keeps P <= 2^15 and enters as the Q K^T chains' initial C; the host runs this
+//     form only while the shift leaves the window [2^-15, 2^15] room for every row (1.13 |q| |k| <= 30), and a row
+//     whose every term still underflowed writes zeros (split: an empty partial), never NaN.
+constexpr int kVStride = 320;
+constexpr int kVBuf = kKBlk * kVStride;  // 20480
+constexpr int kLdsF8 = 2 * kVBuf + 2 * kKBlk * 144;
+
+template <int kKind, int kF8>
+__global__ void __launch_bounds__(kThreads, 2) attn_fwd_f8(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[kLdsF8];
+  static_assert(kF8 == 1 || kF8 == 3, "kF8: 1 fp8 Q K^T, 3 + fp8 P.V with P bytes without exp2");
+  constexpr int KSTR = 144;                 // K LDS row stride (128 B + 16)
+  constexpr int KB1 = kKBlk * KSTR;         // K buffer 1
+  constexpr int VB0 = 2 * kKBlk * KSTR, VB1 = VB0 + kVBuf;
+  constexpr int VSTR8 = 80;                 // kF8 == 3: LDS V^T row stride (64 B + 16: conflict-free ds_read_b128)
+  typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int qb = tile % a.nqb;
+  const int bhs = tile / a.nqb;
+  const int split = bhs % a.nsplit, bh = bhs / a.nsplit;
+  const int b = bh / a.H, h = bh % a.H;
+  const int key0 = split * a.tps * kKBlk;
+  const int Lk = min(a.Lk - key0, a.tps * kKBlk);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int l31 = lane & 31;
+  const int hl = lane >> 5;  // lane half
+  const bool group_b = __builtin_amdgcn_readfirstlane(tid) >= kThreads / 2;
+
+  const char* qp = (const char*)a.q + (b * a.q_sb + h * a.q_sh);
+  const char* kp = (const char*)a.k + (b * a.k_sb + h * a.k_sh + (int64_t)key0 * a.k_sl);
+  const unsigned short* vp = kF8 == 3 ? (const unsigned short*)((const char*)a.v + ((int64_t)bh * a.ntk_v + key0 / kKBlk) * 8192)
+                                      : a.v + b * a.v_sb + h * a.v_sh + (int64_t)key0 * a.v_sl;
+
+  // ---- Q fragments (B operand of S^T = K Q^T): 2 x 32 e4m3 per lane ----
+  const int q_row = qb * kQBlk + wave * kQRows + l31;
+  const int q_row_c = q_row < a.Lq ? q_row : a.Lq - 1;
+  i32x8 qf8[2];
+  {
+    const char* src = qp + (int64_t)q_row_c * a.q_sl + 32 * hl;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(src + 64 * s);
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(src + 64 * s + 16);
+      qf8[s] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+  }
+
+  f32x16 o[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  float l_run = 0.f;
+  const int ntk = (Lk + kKBlk - 1) / kKBlk;
+
+  // staging: group B stages K (a 64 x 128-B tile: 2 chunks of 16 B per thread, rows u/8 + 32 i, chunk u%8); group A
+  // stages V: kF8 == 1 bf16 rows (rows u/16 + 16 i, 4 chunks), kF8 == 3 a v8t tile of 128 d rows x 64 B (8 KiB
+  // contiguous; rows u/4 + 64 i, 2 chunks; whole, v8t pads the last tile with zero keys)
+  const int u = tid & (kThreads / 2 - 1);
+  const bool v8 = kF8 == 3 && !group_b;
+  const int srow = group_b ? u >> 3 : (v8 ? u >> 2 : u >> 4), sch = group_b ? u & 7 : (v8 ? u & 3 : u & 15);
+  const int64_t sl = group_b ? a.k_sl : (v8 ? 64 : a.v_sl);
+  const int esz = (group_b || v8) ? 1 : 2;
+  const char* sbase = group_b ? kp : (const char*)vp;
+  const int st_off = (int)(srow * sl * esz) + sch * 16, st_step = (int)((group_b ? 32 : (v8 ? 64 : 16)) * sl * esz);
+  const int nst = (group_b || v8) ? 2 : 4;
+  u32x4 st[4];
+  auto load_tile = [&](int t) __attribute__((always_inline)) {
+    const int rows = min(Lk - t * kKBlk, kKBlk);
+    const int nbytes = v8 ? (rows > 0 ? 8192 : 0) : (rows > 0 ? (int)((rows - 1) * sl * esz) + esz * kD : 0);
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(sbase + (int64_t)t * (v8 ? 8192 : kKBlk * sl * esz)), (short)0, nbytes, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (i < nst)
+        st[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, st_off + i * st_step, 0, 0));
+  };
+  char* const k_wr = smem + srow * KSTR + sch * 16;
+  char* const v_wr = smem + srow * (kF8 == 3 ? VSTR8 : kVStride) + sch * 16;
+  auto write_k = [&](auto BUF) __attribute__((always_inline)) {
+    constexpr int kb = decltype(BUF)::value ? KB1 : 0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) *reinterpret_cast<u32x4*>(k_wr + kb + 32 * i * KSTR) = st[i];
+  };
+  auto write_v = [&](auto BUF) __attribute__((always_inline)) {
+    constexpr int vb = decltype(BUF)::value ? VB1 : VB0;
+    if constexpr (kF8 == 3) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) *reinterpret_cast<u32x4*>(v_wr + vb + 64 * i * VSTR8) = st[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(v_wr + vb + 16 * i * kVStride) = st[i];
+    }
+  };
+
+  // per-lane LDS read bases
+  const char* const k_rd = smem + l31 * KSTR + 32 * hl;  // + kt*32 rows + 64 s bytes
+  const int grp = lane >> 4, gi = lane & 15;
+  const int tq = gi >> 2, tp = gi & 3;
+  const char* const v_rd = smem + VB0 + (4 * (grp >> 1) + tq) * kVStride + 32 * (grp & 1) + 8 * tp;  // + rows, + 64 db
+  const unsigned v_rd_lds = (unsigned)(uintptr_t)(lds_char_ptr)v_rd;
+  const char* const v_rd8 = smem + VB0 + l31 * VSTR8 + 32 * hl;
+
+  const int ragged_tile = (Lk % kKBlk) != 0 ? Lk / kKBlk : -1;
+
+  f32x16 S[2];   // S^T of the tile awaiting its softmax
+  bf16x8 pb[4];  // kF8 == 1: P^T of the tile awaiting its P.V
+  i32x8 pb8;     // kF8 == 3: the same as e5m2 bytes (byte j = P from S[j >> 4][j & 15])
+  f32x16 sinit;  // -shift in every element (initial C of the Q K^T chains)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) sinit[r] = a.s_init;
+  f32x16 lsum = {};  // kF8 == 3: the row sums, from P^T against an all-ones V^T row
+  const i32x8 ones8 = {0x38383838, 0x38383838, 0x38383838, 0x38383838, 0x38383838, 0x38383838, 0x38383838,
+                       0x38383838};  // e4m3 1.0
+
+  auto k_frag8 = [&](int kb, int kt, int s) __attribute__((always_inline)) {
+    const u32x4 lo = *reinterpret_cast<const u32x4*>(k_rd + kb + kt * 32 * KSTR + 64 * s);
+    const u32x4 hi = *reinterpret_cast<const u32x4*>(k_rd + kb + kt * 32 * KSTR + 64 * s + 16);
+    return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+  };
+  auto v_frag8 = [&](int vb, int db) __attribute__((always_inline)) {  // 32 B of the d row 32 db + l31
+    const u32x4 lo = *reinterpret_cast<const u32x4*>(v_rd8 + vb + 32 * db * VSTR8);
+    const u32x4 hi = *reinterpret_cast<const u32x4*>(v_rd8 + vb + 32 * db * VSTR8 + 16);
+    return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+  };
+  auto qk_mma = [&](auto BUF) __attribute__((always_inline)) {
+    constexpr int kb = decltype(BUF)::value ? KB1 : 0;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+        S[kt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(k_frag8(kb, kt, s), qf8[s], s == 0 ? sinit : S[kt], 0, 0,
+                                                               0, 0, 0, 0);
+  };
+  auto softmax = [&](int t) __attribute__((always_inline)) {
+    if (__builtin_expect(t == ragged_tile, 0)) {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = t * kKBlk + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+          if (key >= Lk) S[kt][r] = -INFINITY;
+        }
+    }
+    asm volatile("" : "+v"(S[0]), "+v"(S[1]));
+    if constexpr (kF8 == 3) {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        unsigned x = 0u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x = __builtin_amdgcn_cvt_pk_u8_f32(fmaf(S[w >> 2][4 * (w & 3) + e], 4.f, 60.f), e, x);
+        pb8[w] = (int)x;
+      }
+      asm volatile("" ::"v"(pb8));
+      return;
+    } else {
+      // contract guard: an overflowed row sum (a norm bound below the real norms) poisons the rows
+      if (__builtin_expect(__any(l_run > 3.0e38f), 0)) {
+        const float nan = __uint_as_float(0x7fc00000u);
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[d][r] = nan;
+      }
+      float psum = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) {
+          bf16x8 v;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float p = __builtin_amdgcn_exp2f(S[kt][8 * sp + j]);
+            psum += p;
+            v[j] = static_cast<__bf16>(p);
+          }
+          pb[2 * kt + sp] = v;
+        }
+      l_run += psum;
+      asm volatile("" ::"v"(pb[0]), "v"(pb[1]), "v"(pb[2]), "v"(pb[3]), "v"(l_run));
+    }
+  };
+
+  typedef std::integral_constant<int, 0> B0;
+  typedef std::integral_constant<int, 1> B1;
+
+  // ---- prologue: K(0), V(0) -> buffer 0; K(1) -> buffer 1; S(0) for everyone, P(0) for A ----
+  load_tile(0);
+  if (group_b) write_k(B0{}); else write_v(B0{});
+  if (group_b) {
+    load_tile(1);
+    write_k(B1{});
+    load_tile(2);
+  } else {
+    load_tile(1);
+  }
+  __syncthreads();
+  qk_mma(B0{});
+  if (!group_b) softmax(0);
+  __syncthreads();
+
+  // one MFMA phase: Q K^T of tile t+1 (4 fp8 MFMAs, compiler-scheduled reads) and P.V of tile t: kF8 == 3 four fp8
+  // MFMAs (+ the row-sum MFMA); kF8 == 1 16 bf16 32x32x16 MFMAs whose V^T operands (two ds_read_b64_tr_b16 each) are
+  // read four MFMAs ahead into a 5-deep ring behind counted lgkmcnt waits
+  auto mfma_phase = [&](auto PAR) __attribute__((always_inline)) {
+    constexpr int par = decltype(PAR)::value;
+    constexpr int kb = (par ^ 1) ? KB1 : 0;  // K(t+1)
+    constexpr int vb = par ? kVBuf : 0;      // V(t), relative to V0
+    __builtin_amdgcn_s_setprio(1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+        S[kt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(k_frag8(kb, kt, s), qf8[s], s == 0 ? sinit : S[kt], 0, 0,
+                                                               0, 0, 0, 0);
+    if constexpr (kF8 == 3) {
+      // P.V(t): A = V^T (e4m3, cbsz 0), B = P^T (e5m2, blgp 1)
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+        o[db] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(v_frag8(vb, db), pb8, o[db], 0, 1, 0, 0, 0, 0);
+      lsum = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ones8, pb8, lsum, 0, 1, 0, 0, 0, 0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_setprio(0);
+      return;
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      bf16x8 ring[5];
+      auto issue = [&](auto JC) __attribute__((always_inline)) {
+        constexpr int j = decltype(JC)::value;
+        if constexpr (j < 16) {
+          constexpr int off = vb + 16 * (j >> 2) * kVStride + 64 * (j & 3);
+          s16x4 lo, hi;
+          asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(v_rd_lds), "i"(off));
+          asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(v_rd_lds), "i"(off + 8 * kVStride));
+          typedef short s16x8 __attribute__((ext_vector_type(8)));
+          const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          ring[j % 5] = __builtin_bit_cast(bf16x8, r);
+        }
+      };
+      static_for<4>(issue);
+      static_for<16>([&](auto JC) __attribute__((always_inline)) {
+        constexpr int j = decltype(JC)::value;
+        issue(std::integral_constant<int, j + 4>{});
+        constexpr int pending = 2 * ((j + 1 < 16) + (j + 2 < 16) + (j + 3 < 16) + (j + 4 < 16));
+        asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(ring[j % 5]) : "i"(pending));
+        o[j & 3] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ring[j % 5], pb[j >> 2], o[j & 3], 0, 0, 0);
+      });
+      __builtin_amdgcn_s_setprio(0);
+    }
+  };
+  if (!group_b) {
+    auto step = [&](auto PAR, int t) __attribute__((always_inline)) {
+      constexpr int par = decltype(PAR)::value;
+      mfma_phase(PAR);
+      __syncthreads();
+      if (t + 1 < ntk) {
+        write_v(std::integral_constant<int, par ^ 1>{});
+        softmax(t + 1);
+        load_tile(t + 2);
+      }
+      __syncthreads();
+    };
+    for (int t = 0; t + 1 < ntk; t += 2) {
+      step(B0{}, t);
+      step(B1{}, t + 1);
+    }
+    if (ntk & 1) step(B0{}, ntk - 1);
+  } else {
+    auto step = [&](auto PAR, int t) __attribute__((always_inline)) {
+      if (t + 2 < ntk) write_k(PAR);
+      softmax(t);
+      if (t + 2 < ntk) load_tile(t + 3);
+      __syncthreads();
+      mfma_phase(PAR);
+      __syncthreads();
+    };
+    for (int t = 0; t + 1 < ntk; t += 2) {
+      step(B0{}, t);
+      step(B1{}, t + 1);
+    }
+    if (ntk & 1) step(B0{}, ntk - 1);
+  }
+
+  // ---- epilogue: O = O^T / l, row q, d = 32db + 8g + 4hl + (0..3); a row whose every term underflowed (l = 0)
+  // is written as zeros / an empty split partial (lse = -inf) instead of 0 * inf = NaN ----
+  const float l_tot = kF8 == 3 ? lsum[0] : wave_swap_sum(l_run);
+  const bool empty = !(l_tot > 0.f);
+  const float inv = empty ? 0.f : (kF8 == 3 ? fmaxf(a.v_amax[bh], 0x1p-100f) * (1.f / 448.f) / l_tot : 1.f / l_tot);
+  if (q_row >= a.Lq) return;
+  if (a.nsplit > 1) {
+    const int64_t row = ((int64_t)(split * a.B + b) * a.H + h) * a.Lq + q_row;
+    float* op = a.o_part + row * kD;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        f32x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = o[db][4 * gg + e] * inv;
+        *reinterpret_cast<f32x4*>(op + 32 * db + 8 * gg + 4 * hl) = w;
+      }
+    if (hl == 0) a.lse_part[row] = empty ? -INFINITY : -a.s_init + __log2f(l_tot);
+    return;
+  }
+  unsigned short* op = a.o + b * a.o_sb + h * a.o_sh + (int64_t)q_row * a.o_sl;
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      u16x4 w;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w[e] = f2bf(o[db][4 * gg + e] * inv);
+      *reinterpret_cast<u16x4*>(op + 32 * db + 8 * gg + 4 * hl) = w;
+    }
+}
+
+// O[b, q, h, :] = sum_s w_s O_s / sum_s w_s with w_s = exp2(lse_s - max_s lse_s): the key-range partials of one
+// (b, h, q) row combined exactly as the online softmax would have (empty partials carry lse = -inf, weight 0).
+// One thread per 4 head-dim elements (32 threads per row); HBM-bound.
+__global__ void __launch_bounds__(256) attn_merge_splits(const float* __restrict__ o_part,
+                                                        const float* __restrict__ lse_part, unsigned short* o,
+                                                        int nsplit, int B, int H, int Lq, int64_t o_sb,
+                                                        int64_t o_sl, int64_t o_sh) {
+  const int64_t rows = (int64_t)B * H * Lq;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t row = gid >> 5;
+  if (row >= rows) return;
+  const int d = (int)(gid & 31) * 4;
+  float mx = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) mx = fmaxf(mx, lse_part[s * rows + row]);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float den = 0.f;
+  for (int s = 0; s < nsplit; ++s) {
+    const float l = lse_part[s * rows + row];
+    if (!(l > -INFINITY)) continue;
+    const float w = __builtin_amdgcn_exp2f(l - mx);
+    const f32x4 v = *reinterpret_cast<const f32x4*>(o_part + (s * rows + row) * kD + d);
+    acc += w * v;
+    den += w;
+  }
+  const float inv = den > 0.f ? 1.f / den : 0.f;
+  const int q = (int)(row % Lq);
+  const int bh = (int)(row / Lq);
+  const int b = bh / H, h = bh % H;
+  u16x4 w;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) w[e] = f2bf(acc[e] * inv);
+  *reinterpret_cast<u16x4*>(o + b * o_sb + (int64_t)q * o_sl + h * o_sh + d) = w;
+}
+
+int g_num_cus = 0;
+int num_cus() {
+  if (g_num_cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    g_num_cus = n;
+  }
+  return g_num_cus;
+}
+
+// Work-balance model for the key-range split: the kernel holds one workgroup per CU (2 waves/SIMD), every
+// workgroup's time is ~ its key tiles + a fixed ~44 tiles, and workgroups run in ceil(nwg / CUs) rounds; a split
+// adds the fp32 partial write + merge traffic (~1 tile of time per 9 MB at HBM rate). The fixed cost is fitted to
+// MI355X measurements (tools/bench_cp_chunks.py: B 2, H 16, Lq 13640, Lk 109120 ran 21.9 ms unsplit vs 23.0 ms at
+// split 4; H 4: 6.24 vs 6.14 ms): shorter workgroups lose the lock-step K/V streaming through the XCD's L2 that
+// long ones keep. Picks the split with the least modelled time.
+int plan_split(int B, int H, int Lq, int Lk) {
+  const int64_t nqb = cdiv(Lq, kQBlk), ntiles = cdiv(Lk, kKBlk);
+  const int64_t nwg = nqb * B * H, cus = num_cus();
+  int best = 1;
+  double best_cost = 1e300;
+  for (int s = 1; s <= 8 && s <= ntiles; ++s) {
+    const int64_t tps = cdiv(ntiles, s);
+    if (cdiv(ntiles, tps) != s) continue;  // every split must own at least one tile
+    const double rounds = (double)cdiv(nwg * s, cus);
+    double cost = rounds * (double)(tps + 44);
+    if (s > 1) cost += (2.0 * s + 0.5) * (double)B * H * Lq * kD * 4 / 9.0e6;
+    if (cost < best_cost * 0.995) { best_cost = cost; best = s; }
+  }
+  return best;
+}
+
+// The m16 softmax-shift mode for these bounds (the bound product in log2 units; |q_row| <= q_norm_bound): 1 zero
+// shift (pre-scaled q, product <= 96), 0 fixed per-row shift (product <= 98), 2 online max (larger or unknown)
+int m16_mode(float q_norm_bound, float k_norm_bound, float scale_log2, bool prescaled) {
+  const double bb = (double)q_norm_bound * k_norm_bound * (prescaled ? 1.0 : scale_log2);
+  if (!(q_norm_bound > 0.f && k_norm_bound > 0.f) || bb > kMaxBound) return 2;
+  return prescaled && bb <= kTop ? 1 : 0;
+}
+
+// Short-key (text cross-attention) launches: 1 = the persistent form (attn_fwd_m16<.., kPersist>), 0 = one workgroup
+// per block. Set only through cp25_attn_cross_select (never read from the environment).
+int g_xattn_form = 1;
+
+// the persistent form runs unsplit cross-attention launches in the zero-shift and online modes with >= 2 key tiles
+bool use_xattn_persistent(bool short_keys, int n_split, int mode, int64_t ntiles) {
+  return g_xattn_form == 1 && short_keys && n_split == 1 && mode != 0 && ntiles >= 2;
+}
+
+}  // namespace
+
+extern "C" int cp25_attn_cross_select(int form) {
+  if (form != 0 && form != 1) return CP25_ERR_INVAL;
+  const int prev = g_xattn_form;
+  g_xattn_form = form;
+  return prev;
+}
+
+// fp8: 0 bf16; 1 = Q K^T on e4m3 q / k; 2 = also P.V on e5m2 P and the e4m3 v8t layout (v = v8t, v_strides unused)
+static int attn_launch(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq, int Lk, int D,
+                       const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
+                       const int64_t* o_strides, float softmax_scale, float q_norm_bound, float k_norm_bound,
+                       int n_split, void* workspace, size_t ws_bytes, hipStream_t stream, bool prescaled = false,
+                       int fp8 = 0, const float* v_amax = nullptr, const float* kslots = nullptr, int n_kslots = 0) {
+  const bool fp8qk = fp8 >= 1;
+  if (D != kD) return CP25_ERR_DTYPE;
+  if (fp8qk && !prescaled) return CP25_ERR_INVAL;
+  if (fp8 == 2 && (!v_amax || ((uintptr_t)v_amax & 3))) return CP25_ERR_INVAL;
+  // fp8 Q K^T: P = exp2(S) with no shift needs every score inside [-60, 60]
+  if (fp8qk && !(q_norm_bound > 0.f && k_norm_bound > 0.f && (double)q_norm_bound * k_norm_bound <= (double)kTopF8))
+    return CP25_ERR_INVAL;
+  // fp8 P.V: the e5m2 window [2^-15, 2^15] must hold a term of every row (shift 1.13 qb kb - 15 <= 15)
+  if (fp8 == 2 && 1.13 * (double)q_norm_bound * k_norm_bound > 30.0) return CP25_ERR_INVAL;
+  if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0) return CP25_ERR_INVAL;
+  if (!q || !k || !v || !o) return CP25_ERR_INVAL;
+  if (!(softmax_scale > 0.f) || !(q_norm_bound >= 0.f) || !(k_norm_bound >= 0.f) || q_norm_bound > 1e18f ||
+      k_norm_bound > 1e18f)
+    return CP25_ERR_INVAL;
+  // rows must be 16-byte aligned for the vector loads / stores; head dim contiguous
+  const int64_t* ss[4] = {q_strides, k_strides, v_strides, o_strides};
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 3; ++j)
+      if (!(fp8 == 2 && i == 2) && ss[i][j] % (fp8qk && i < 2 ? 16 : 8) != 0) return CP25_ERR_INVAL;
+  // buffer_load offsets within a 64-key tile are 32-bit
+  if ((int64_t)kKBlk * k_strides[1] * (fp8qk ? 1 : 2) >= (1ll << 31) ||
+      (fp8 != 2 && (int64_t)kKBlk * v_strides[1] * 2 >= (1ll << 31)))
+    return CP25_ERR_INVAL;
+  if (k_strides[1] <= 0 || (fp8 != 2 && v_strides[1] <= 0)) return CP25_ERR_INVAL;
+  if (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) & 15) return CP25_ERR_INVAL;
+  const int64_t ntiles = cdiv(Lk, kKBlk);
+  if (n_split < 1 || n_split > ntiles) return CP25_ERR_INVAL;
+  const int64_t tps = cdiv(ntiles, n_split);
+  if (cdiv(ntiles, tps) != n_split) return CP25_ERR_INVAL;  // a split without keys
+  const int64_t rows = (int64_t)B * H * Lq;
+  if (n_split > 1) {
+    if (!workspace || ((uintptr_t)workspace & 15) || ws_bytes < cp25_attn_workspace_bytes(B, H, Lq, n_split))
+      return CP25_ERR_INVAL;
+  }
+  AttnArgs a;
+  a.q = (const unsigned short*)q; a.k = (const unsigned short*)k; a.v = (const unsigned short*)v;
+  a.o = (unsigned short*)o;
+  a.q_sb = q_strides[0]; a.q_sl = q_strides[1]; a.q_sh = q_strides[2];
+  a.k_sb = k_strides[0]; a.k_sl = k_strides[1]; a.k_sh = k_strides[2];
+  a.v_sb = v_strides[0]; a.v_sl = v_strides[1]; a.v_sh = v_strides[2];
+  a.o_sb = o_strides[0]; a.o_sl = o_strides[1]; a.o_sh = o_strides[2];
+  a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk;
+  a.nqb = (int)cdiv(Lq, kQBlk);
+  a.nsplit = n_split;
+  a.tps = (int)tps;
+  a.ntk_v = (int)ntiles;
+  a.v_amax = v_amax;
+  // fp8 P.V: P = exp2(S - shift) <= 2^15 (e5m2 max 57344 = 2^15.8) for every score the norm bounds allow, with the
+  // e4m3 rounding of q and k (each element within 2^-4 relative: |q8| |k8| <= 1.13 |q| |k|)
+  a.s_init = fp8 == 2 ? -std::max(0.f, 1.13f * q_norm_bound * k_norm_bound - 15.f) : 0.f;
+  a.o_part = n_split > 1 ? (float*)workspace : nullptr;
+  a.lse_part = n_split > 1 ? (float*)workspace + (size_t)n_split * rows * kD : nullptr;
+  a.scale_log2 = prescaled ? 1.f : softmax_scale * 1.4426950408889634f;
+  a.kbound = q_norm_bound > 0.f ? k_norm_bound : 0.f;  // a missing q bound: online (the kernel measures |q_row|)
+  a.kslots = kslots;
+  a.n_kslots = n_kslots;
+  const int64_t nwg = (int64_t)a.nqb * B * H * n_split;
+  if (nwg > 0x7fffffff) return CP25_ERR_INVAL;
+  const bool xk = Lk <= 4096;  // short-key launches (text cross-attention) get their own symbol in profiles
+  if (fp8 == 2) {
+    hipLaunchKernelGGL((xk ? attn_fwd_f8<1, 3> : attn_fwd_f8<0, 3>), dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
+  } else if (fp8qk) {
+    hipLaunchKernelGGL((xk ? attn_fwd_f8<1, 1> : attn_fwd_f8<0, 1>), dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
+  } else {
+    const int mode = m16_mode(q_norm_bound, k_norm_bound, a.scale_log2, prescaled);
+    void (*kern)(AttnArgs) = nullptr;
+    int64_t grid = nwg;
+    if (prescaled && kslots && mode != 1) {
+      // the gated pair: blocks whose data-tight bound allows it run the zero-shift loop, the others the online max
+      hipLaunchKernelGGL((xk ? attn_fwd_m16<1, true, 1, false, 1> : attn_fwd_m16<0, true, 1, false, 1>),
+                         dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
+      CP25_LAUNCH_CHECK();
+      kern = xk ? attn_fwd_m16<1, true, 2, false, 2> : attn_fwd_m16<0, true, 2, false, 2>;
+    } else if (use_xattn_persistent(xk, n_split, mode, ntiles)) {
+      // one workgroup per CU over contiguous runs of blocks (every workgroup gets at least one)
+      grid = std::min<int64_t>(nwg, num_cus());
+      if (prescaled) kern = mode == 2 ? attn_fwd_m16<1, true, 2, true> : attn_fwd_m16<1, true, 1, true>;
+      else kern = attn_fwd_m16<1, false, 2, true>;
+    } else {
+#define M16(P, M) kern = xk ? attn_fwd_m16<1, P, M> : attn_fwd_m16<0, P, M>
+      if (prescaled) {
+        if (mode == 2) M16(true, 2); else if (mode == 1) M16(true, 1); else M16(true, 0);
+      } else {
+        if (mode == 2) M16(false, 2); else M16(false, 0);
+      }
+#undef M16
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kThreads), 0, stream, a);
+  }
+  CP25_LAUNCH_CHECK();
+  if (n_split > 1) {
+    const int64_t threads = rows * 32;
+    hipLaunchKernelGGL(attn_merge_splits, dim3((unsigned)cdiv(threads, 256)), dim3(256), 0, stream, a.o_part,
+                       a.lse_part, a.o, n_split, B, H, Lq, a.o_sb, a.o_sl, a.o_sh);
+    CP25_LAUNCH_CHECK();
+  }
+  return CP25_OK;
+}
+
+extern "C" int cp25_attn_fwd_prescaled_fp8qk(const void* q8, const void* k8, const void* v, void* o, int B, int H,
+                                             int Lq, int Lk, int D, const int64_t* q_strides,
+                                             const int64_t* k_strides, const int64_t* v_strides,
+                                             const int64_t* o_strides, float q_norm_bound, float k_norm_bound,
+                                             int n_split, void* workspace, size_t ws_bytes, hipStream_t stream) {
+  return attn_launch(q8, k8, v, o, B, H, Lq, Lk, D, q_strides, k_strides, v_strides, o_strides, 0.6931471805599453f,
+                     q_norm_bound, k_norm_bound, n_split, workspace, ws_bytes, stream, true, 1);
+}
+
+extern "C" int cp25_attn_fwd_prescaled_fp8(const void* q8, const void* k8, const void* v8t, const float* v_amax,
+                                           void* o, int B, int H, int Lq, int Lk, int D, const int64_t* q_strides,
+                                           const int64_t* k_strides, const int64_t* o_strides, float q_norm_bound,
+                                           float k_norm_bound, int n_split, void* workspace, size_t ws_bytes,
+                                           hipStream_t stream) {
+  const int64_t none[3] = {0, 0, 0};
+  return attn_launch(q8, k8, v8t, o, B, H, Lq, Lk, D, q_strides, k_strides, none, o_strides, 0.6931471805599453f,
+                     q_norm_bound, k_norm_bound, n_split, workspace, ws_bytes, stream, true, 2, v_amax);
+}
+
+extern "C" size_t cp25_attn_workspace_bytes(int B, int H, int Lq, int n_split) {
+  if (n_split <= 1 || B <= 0 || H <= 0 || Lq <= 0) return 0;
+  return (size_t)n_split * B * H * Lq * (kD + 1) * sizeof(float);
+}
+
+extern "C" int cp25_attn_plan(int B, int H, int Lq, int Lk, int D) {
+  if (D != kD) return CP25_ERR_DTYPE;
+  if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0) return CP25_ERR_INVAL;
+  return plan_split(B, H, Lq, Lk);
+}
+
+extern "C" int cp25_attn_fwd(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq,
+                             int Lk, int D, const int64_t* q_strides, const int64_t* k_strides,
+                             const int64_t* v_strides, const int64_t* o_strides, float softmax_scale,
+                             hipStream_t stream) {
+  return attn_launch(q, k, v, o, B, H, Lq, Lk, D, q_strides, k_strides, v_strides, o_strides, softmax_scale, 0.f,
+                     0.f, 1, nullptr, 0, stream);
+}
+
+extern "C" int cp25_attn_fwd_split(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq,
+                                   int Lk, int D, const int64_t* q_strides, const int64_t* k_strides,
+                                   const int64_t* v_strides, const int64_t* o_strides, float softmax_scale,
+                                   int n_split, void* workspace, size_t ws_bytes, hipStream_t stream) {
+  return attn_launch(q, k, v, o, B, H, Lq, Lk, D, q_strides, k_strides, v_strides, o_strides, softmax_scale, 0.f,
+                     0.f, n_split, workspace, ws_bytes, stream);
+}
+
+extern "C" int cp25_attn_fwd_bounded(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq,
+                                     int Lk, int D, const int64_t* q_strides, const int64_t* k_strides,
+                                     const int64_t* v_strides, const int64_t* o_strides, float softmax_scale,
+                                     float q_norm_bound, float k_norm_bound, int n_split, void* workspace,
+                                     size_t ws_bytes, hipStream_t stream) {
+  return attn_launch(q, k, v, o, B, H, Lq, Lk, D, q_strides, k_strides, v_strides, o_strides, softmax_scale,
+                     q_norm_bound, k_norm_bound, n_split, workspace, ws_bytes, stream);
+}
+
+extern "C" int cp25_attn_fwd_prescaled(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq,
+                                       int Lk, int D, const int64_t* q_strides, const int64_t* k_strides,
+                                       const int64_t* v_strides, const int64_t* o_strides, float q_norm_bound,
+                                       float k_norm_bound, int n_split, void* workspace, size_t ws_bytes,
+                                       hipStream_t stream) {
+  return attn_launch(q, k, v, o, B, H, Lq, Lk, D, q_strides, k_strides, v_strides, o_strides, 0.6931471805599453f,
+                     q_norm_bound, k_norm_bound, n_split, workspace, ws_bytes, stream, true);
+}
+
+extern "C" int cp25_attn_fwd_prescaled_kslots(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq,
+                                              int Lk, int D, const int64_t* q_strides, const int64_t* k_strides,
+                                              const int64_t* v_strides, const int64_t* o_strides, float q_norm_bound,
+                                              float k_norm_bound, const float* k_norm_slots, int n_slots, int n_split,
+                                              void* workspace, size_t ws_bytes, hipStream_t stream) {
+  if (!k_norm_slots || n_slots < 1 || n_slots > 64 || ((uintptr_t)k_norm_slots & 3)) return CP25_ERR_INVAL;
+  return attn_launch(q, k, v, o, B, H, Lq, Lk, D, q_strides, k_strides, v_strides, o_strides, 0.6931471805599453f,
+                     q_norm_bound, k_norm_bound, n_split, workspace, ws_bytes, stream, true, 0, nullptr, k_norm_slots,
+                     n_slots);
+}
+
+extern "C" const char* cp25_attn_kernel(int Lk, float softmax_scale, float q_norm_bound, float k_norm_bound,
+                                        int prescaled, int fp8) {
+  if (prescaled == 2 && m16_mode(q_norm_bound, k_norm_bound, 1.f, true) != 1)  // cp25_attn_fwd_prescaled_kslots
+    return Lk <= 4096 ? "attn_fwd_m16<cross, prescaled, gated zero shift | online max>"
+                      : "attn_fwd_m16<self, prescaled, gated zero shift | online max>";
+  if (fp8 == 2) return Lk <= 4096 ? "attn_fwd_f8<cross, fp8 Q K^T + fp8 P.V>" : "attn_fwd_f8<self, fp8 Q K^T + fp8 P.V>";
+  if (fp8 == 1) return Lk <= 4096 ? "attn_fwd_f8<cross, fp8 Q K^T>" : "attn_fwd_f8<self, fp8 Q K^T>";
+  if (Lk <= 4096) {
+    const float sl = prescaled ? 1.f : softmax_scale * 1.4426950408889634f;
+    const int mode = m16_mode(q_norm_bound, k_norm_bound, sl, prescaled != 0);
+    if (use_xattn_persistent(true, 1, mode, cdiv(Lk, kKBlk)))
+      return mode == 1 ? "attn_fwd_m16<cross, prescaled, zero shift, persistent>"
+                       : (prescaled ? "attn_fwd_m16<cross, prescaled, online max, persistent>"
+                                    : "attn_fwd_m16<cross, online max, persistent>");
+  }
+  static const char* names[2][2][3] = {
+      {{"attn_fwd_m16<self, fixed shift>", "?", "attn_fwd_m16<self, online max>"},
+       {"attn_fwd_m16<self, prescaled, fixed shift>", "attn_fwd_m16<self, prescaled, zero shift>",
+        "attn_fwd_m16<self, prescaled, online max>"}},
+      {{"attn_fwd_m16<cross, fixed shift>", "?", "attn_fwd_m16<cross, online max>"},
+       {"attn_fwd_m16<cross, prescaled, fixed shift>", "attn_fwd_m16<cross, prescaled, zero shift>",
+        "attn_fwd_m16<cross, prescaled, online max>"}}};
+  const float sl = prescaled ? 1.f : softmax_scale * 1.4426950408889634f;
+  return names[Lk <= 4096][prescaled != 0][m16_mode(q_norm_bound, k_norm_bound, sl, prescaled != 0)];
+}
