@@ -37,3 +37,28 @@ def test_self_attention_loop_shape():
     # MFMA / softmax phases: at most the one reload + one spill of the NaN fill
     assert r["inloop_scratch"] <= 2, r["inloop_scratch"]
     assert r["nops"] <= 40, r["nops"]  # 192 with the operand-redefining wait pins
+
+
+_SYNTH = """_Zk:
+\tds_read_b128 v[0:3], v10
+\ts_cbranch_scc1 .LBB0_2
+\ts_waitcnt lgkmcnt(0)
+\ts_branch .LBB0_3
+.LBB0_1:
+\tv_add_f32_e32 v20, v1, v21
+\ts_endpgm
+.LBB0_2:
+\tv_add_f32_e32 v22, v2, v23
+.LBB0_3:
+\tv_mov_b32_e32 v3, v24
+\ts_endpgm
+.Lfunc_end0:
+"""
+
+
+def test_race_check_follows_control_flow():
+    """The checker on a hand-made stream: the read of v[0:3] is retired on the fall-through path only, so v2 on the
+    branch target is a race and so is v3 where both paths join; the block after the unconditional branch is reached
+    by no path with the read in flight (no race there: the checker's linear form reported one)."""
+    r = isa_check.analyse(_SYNTH, "_Zk")
+    assert r["races"] == ["v_add_f32_e32 v22, v2, v23", "v_mov_b32_e32 v3, v24"]

@@ -2,7 +2,7 @@
 """Static checks of the gfx950 ISA of a HIP source (hipcc --cuda-device-only -S): per kernel, VGPRs / spills (the
 compiler's resource remarks), in-loop scratch and vmcnt(0), s_nop count, and LDS-read races: an instruction that reads
 or writes a VGPR while an LDS read into it is still in flight (not yet retired by an s_waitcnt lgkmcnt, counted in
-issue order). The hand-scheduled kernels issue ds_reads from inline asm whose destinations the compiler does not know
+issue order, joined over the control-flow graph's paths). The hand-scheduled kernels issue ds_reads from inline asm whose destinations the compiler does not know
 are written asynchronously; if such an asm output is dead (e.g. its MFMA was eliminated) the register allocator may
 hand the register to another value while the read is in flight -- a silent wrong result this check catches.
 usage: python tools/isa_check.py file.hip [name-filter]   (exit 1 on any race)"""
@@ -45,18 +45,34 @@ def _regs(op):
     return {int(m.group(1))} if m else set()
 
 
+def _merge(a, b):
+    """Join of two in-flight LDS-read queues (oldest first), aligned at the newest entry: an lgkmcnt(n) wait keeps the
+    newest n entries, so entry k from the end means the same thing on both paths."""
+    n = max(len(a), len(b))
+    a = [set()] * (n - len(a)) + list(a)
+    b = [set()] * (n - len(b)) + list(b)
+    return [x | y for x, y in zip(a, b)][-32:]
+
+
 def analyse(asm, name):
+    """Per kernel: races found by a dataflow over the control-flow graph (each instruction's in-flight LDS reads are the
+    join over its predecessors: fall-through, unless the previous instruction is an unconditional branch or the end of
+    the program, and every branch to its label), s_nop count, and in-loop scratch / vmcnt(0) counts."""
     i = asm.index(name + ":")
     j = asm.index(".Lfunc_end", i)
     lines = asm[i:j].split("\n")
-    pending, races, nops = [], [], 0
+    ins, labels, nops = [], {}, 0
     inloop, scr, vm0 = False, 0, 0
     for l in lines:
         s = l.strip()
         if not s or s.startswith(";"):
             continue
-        if re.match(r"^\.LBB", l):
+        m = re.match(r"^(\.LBB\S+):", l)
+        if m:
             inloop = "Loop" in l
+            labels[m.group(1)] = len(ins)
+            continue
+        if s.startswith("."):
             continue
         t = s.replace(",", " ").split()
         op = t[0]
@@ -66,6 +82,24 @@ def analyse(asm, name):
             vm0 += 1
         if op == "s_nop":
             nops += 1
+        ins.append((op, t, s))
+    succ = []
+    for k, (op, t, s) in enumerate(ins):
+        nxt = []
+        if op.startswith("s_cbranch") or op == "s_branch":
+            if len(t) > 1 and t[1] in labels:
+                nxt.append(labels[t[1]])
+        if op not in ("s_branch", "s_endpgm", "s_setpc_b64") and k + 1 < len(ins):
+            nxt.append(k + 1)
+        succ.append(nxt)
+    state = [None] * len(ins)
+    state[0] = []
+    work = [0]
+    races = set()
+    while work:
+        k = work.pop()
+        op, t, s = ins[k]
+        pending = [set(x) for x in state[k]]
         if op.startswith("ds_read"):
             pending.append(_regs(t[1]))
         elif op.startswith(("ds_", "s_load", "s_buffer_load")):
@@ -74,16 +108,20 @@ def analyse(asm, name):
             m = re.search(r"lgkmcnt\((\d+)\)", s)
             if m:
                 n = int(m.group(1))
-                while len(pending) > n:
-                    pending.pop(0)
+                pending = pending[len(pending) - n:] if len(pending) > n else pending
         else:
             live = set().union(*pending) if pending else set()
             used = set()
             for x in t[1:]:
                 used |= _regs(x)
             if used & live:
-                races.append(s)
-    return {"races": races, "nops": nops, "inloop_scratch": scr, "inloop_vmcnt0": vm0}
+                races.add((k, s))
+        for q in succ[k]:
+            new = pending if state[q] is None else _merge(state[q], pending)
+            if state[q] is None or new != state[q]:
+                state[q] = new
+                work.append(q)
+    return {"races": [s for _, s in sorted(races)], "nops": nops, "inloop_scratch": scr, "inloop_vmcnt0": vm0}
 
 
 def check(src, flt=""):
