@@ -5,12 +5,13 @@ Instruction j of group-B wave w covers K-buffer bytes [1024 (w + 4 j), +1024) (1
 5, waves 2-3 issue 4); lane l moves the 16 B at byte 16 l of it: row b / 288, column b % 288 (columns >= 256 are the
 row padding: they re-read the tile's first 16 B). Rows past Lk on the ragged tile read row rows - 1 (their scores are
 masked to -inf). Only the per-block kernels (not the persistent form) take this path.
-usage: make_dmak.py [kv]   (kv: group A's V tiles too, issued at the start of its softmax phase, waited before the
+usage: make_dmak.py [kv|mode]   (mode: K always, V in the online-max form only)   (kv: group A's V tiles too, issued at the start of its softmax phase, waited before the
 barrier that closes it; rows past Lk read row rows - 1, finite, under P = 0) -> /tmp/attn_dmak[v].hip"""
 import os
 import sys
 
-KV = len(sys.argv) > 1 and sys.argv[1] == "kv"
+KV = len(sys.argv) > 1 and sys.argv[1] in ("kv", "mode")
+MODE = len(sys.argv) > 1 and sys.argv[1] == "mode"
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 src = open(os.path.join(ROOT, "cosmos-predict2.5_amd", "csrc", "attn_fwd.hip")).read()
@@ -127,6 +128,21 @@ if KV:
       }
       if constexpr (kDmaK) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();""")
-out = "/tmp/attn_dmakv.hip" if KV else "/tmp/attn_dmak.hip"
+if MODE:
+    rep("""  } else if (kDmaK) {
+    dma_k(0, B0{});  // V(0)""", """  } else if (kDmaV) {
+    dma_k(0, B0{});  // V(0)""")
+    rep("""        if constexpr (kDmaK) {
+          dma_k(t + 1, std::integral_constant<int, par ^ 1>{});  // V(t+1): buffer free since the last barrier""",
+        """        if constexpr (kDmaV) {
+          dma_k(t + 1, std::integral_constant<int, par ^ 1>{});  // V(t+1): buffer free since the last barrier""")
+    rep("""      if constexpr (kDmaK) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();""", """      if constexpr (kDmaV) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();""")
+    rep("""  constexpr bool kDmaK = !kPersist;
+""", """  constexpr bool kDmaK = !kPersist;
+  constexpr bool kDmaV = kDmaK && kMode == 2;  // V too in the online form (zero shift: K only, measured)
+""")
+out = "/tmp/attn_dmakmode.hip" if MODE else ("/tmp/attn_dmakv.hip" if KV else "/tmp/attn_dmak.hip")
 open(out, "w").write(src)
 print(out)
