@@ -8,9 +8,11 @@ One bench *step* = one full-geometry sampler evaluation (SamplingRun.step(): pat
 replacement, the CFG-batched B = 2 DiT forward on the 2B net at latent [16, 31, 88, 160],
 L = 109 120 tokens, GT-frame velocity replacement + CFG, fused UniPC update). The encode, the setup
 and the 121-frame decode are timed once each in the same run (barrier + synchronize around each);
-  value = frames / (t_encode + t_setup + evals_per_video * t_step + t_decode)
-i.e. whole-video frames/s. Synthetic data: seeded random weights with the 2B shapes, a random
-conditioning image, N(0, 1) text embeddings [1, 512, 100352]. bf16 compute.
+  modeled = frames / (t_encode + t_setup + evals_per_video * t_step + t_decode)
+and, by default, one whole video is then timed end to end (encode + every evaluation + decode, barrier +
+synchronize around it): value = frames / t_whole_video (--no-whole-video: value = the modeled figure).
+Synthetic data: seeded random weights with the 2B shapes, a random conditioning image, N(0, 1) text
+embeddings [1, 512, 100352]. bf16 compute.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
 N > 1 (one rank per GPU, RCCL; under torch.distributed.run, or started by bench.py itself when launched plainly): the video's token sequence is sharded context-parallel over
@@ -61,16 +63,17 @@ def parse():
     ap.add_argument("--norm-weights", default="",
                     help="lo,hi: every q/k RMSNorm weight uniform in [lo, hi] (seeded) instead of the init's ones -- the "
                          "attention then runs the form a trained checkpoint gets (the report names it)")
-    ap.add_argument("--whole-video", action="store_true",
-                    help="also time one whole video end to end (encode + all evaluations + decode) and report it next "
-                         "to the per-evaluation value")
+    ap.add_argument("--no-whole-video", action="store_true",
+                    help="skip the end-to-end video (value is then the per-evaluation model; for quick A/B runs)")
     ap.add_argument("--block-gemm", default="own", choices=("own", "lib"),
                     help="bf16 block projections: own = the hand-written MFMA GEMM with fused GELU / gated-residual "
                          "epilogues (default), lib = hipBLASLt + the elementwise kernels (A/B)")
     ap.add_argument("--no-cfg-share", action="store_true",
                     help="every CFG entry computes block 0's shared self-attention prefix (A/B of the sharing)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (0: the host cores this process may use, capped by OMP_NUM_THREADS)")
+    ap.add_argument("--no-cpu-config1", action="store_true", help="skip the CPU baseline's config-1 end-to-end video")
     ap.add_argument("--backend", default="nccl", help="process-group backend for N > 1 (nccl = RCCL; gloo only "
                     "for rehearsing the multi-rank flow with several ranks on one GPU, see --share-device)")
     ap.add_argument("--share-device", action="store_true", help="every rank uses cuda:0 (rehearsal on one GPU)")
@@ -211,16 +214,18 @@ def main():
         advance(a.warmup)
         net = model.net
         net.attn_events = []
+        net.comm_events = [] if world > 1 else None
         _, t_steps = timer(lambda: advance(a.steps))
         ev = net.attn_events
-        net.attn_events = None
+        cev = net.comm_events
+        net.attn_events = net.comm_events = None
         t_step = t_steps / a.steps
         lat = run.latents()
         video, t_dec = timer(lambda: model.decode(lat))
         assert video.shape[2] == frames and torch.isfinite(video.float()).all()
         del video
         t_whole = None
-        if a.whole_video:
+        if not a.no_whole_video:
             def whole():
                 g0 = model.encode_conditioning(batch["video"], 1, state_t)
                 r0 = model.begin_sampling(g0, batch["t5_text_embeddings"], batch["neg_t5_text_embeddings"],
@@ -244,13 +249,30 @@ def main():
     attn_avg_s = (sum(attn_ms) / len(attn_ms)) / 1e3 if attn_ms else float("nan")
     achieved = attn_flop / attn_avg_s / 1e12 if attn_ms else 0.0
 
+    # context parallel: per rank, the exposed K/V gather waits (HIP events on the compute stream around each wait) and
+    # the self-attention launches of the timed steps, per evaluation
+    cp_report = None
+    if world > 1:
+        mine = {"rank": rank, "gather_wait_ms_per_eval": sum(e0.elapsed_time(e1) for e0, e1 in cev) / a.steps,
+                "gather_waits_per_eval": len(cev) / a.steps,
+                "attention_ms_per_eval": sum(e0.elapsed_time(e1) for e0, e1, _ in ev) / a.steps,
+                "eval_ms": t_step * 1e3}
+        every = [None] * world
+        dist.all_gather_object(every, mine)
+        cp_report = {"per_rank": every,
+                     "max_gather_wait_ms_per_eval": max(r["gather_wait_ms_per_eval"] for r in every),
+                     "max_attention_ms_per_eval": max(r["attention_ms_per_eval"] for r in every)}
+
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         sys.path.insert(0, ROOT)
-        from oracle.cpu_baseline import dit_block_sample
+        from oracle.cpu_baseline import config1_end_to_end, dit_block_sample, host_threads
 
-        cpu = dit_block_sample(L=state_t * (h // 16) * (w // 16), threads=a.cpu_threads,
-                               forwards=2 * evals, frames=frames)
+        threads, visible = host_threads(a.cpu_threads or None)
+        cpu = dit_block_sample(L=state_t * (h // 16) * (w // 16), threads=threads, forwards=2 * evals, frames=frames)
+        cpu["host_cores_visible"] = visible
+        if not a.no_cpu_config1:
+            cpu["config1_end_to_end"] = config1_end_to_end(threads=threads)
 
     if rank == 0:
         valid = (a.num_steps == 35 and a.frames == 121 and (h, w) == (704, 1280) and a.model == "2B/post-trained"
@@ -263,9 +285,10 @@ def main():
             with open(PMC_SUMMARY) as f:
                 traffic = json.load(f).get("traffic_bytes_per_launch")
             traffic_src = "static prior: " + os.path.relpath(PMC_SUMMARY, ROOT) + " (rocprofv3 PMC, not this run)"
+        modeled = frames / video_s
         line = {
             "metric": METRIC,
-            "value": frames / video_s,
+            "value": frames / t_whole if t_whole is not None else modeled,
             "unit": "frames/s",
             "n_gpus": world,
             "steps": a.steps,
@@ -281,9 +304,12 @@ def main():
                      + " + bf16",
             "data": "synthetic: seeded random 2B/VAE weights, random conditioning image, N(0,1) text embeddings"
                     + (f", q/k norm weights uniform in [{a.norm_weights}]" if a.norm_weights else ""),
-            "value_method": "per-evaluation timing: frames / (encode + setup + evals x mean timed evaluation + decode), "
-                            "each part timed in this run",
+            "value_method": ("whole video timed end to end in this run (encode + every evaluation + decode)"
+                             if t_whole is not None else
+                             "per-evaluation model: frames / (encode + setup + evals x mean timed evaluation + decode), "
+                             "each part timed in this run"),
             "whole_video": None if t_whole is None else {"seconds": t_whole, "frames_per_s": frames / t_whole},
+            "modeled_value": modeled,
             "config": {
                 "workload": f"Predict2.5-2B Image2World {h}x{w}x{frames}f ({a.model}), {a.num_steps} "
                             + (f"Karras UniPC steps ({evals} evals" if karras else f"shift-5 UniPC steps ({evals} evals")
@@ -330,8 +356,11 @@ def main():
                 "avg_launch_ms": attn_avg_s * 1e3,
                 "flop_per_launch": attn_flop,
             },
-            "cpu_baseline": cpu and {k: cpu[k] for k in ("value", "unit", "cores", "kind", "sample")},
+            "cpu_baseline": cpu and {k: cpu[k] for k in ("value", "unit", "cores", "kind", "sample", "host_cores_visible",
+                                                         "sample_seconds", "config1_end_to_end") if k in cpu},
         }
+        if cp_report is not None:
+            line["context_parallel"] = cp_report
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -430,6 +430,12 @@ def gemm_supported(N: int, K: int) -> bool:
     return N % 256 == 0 and K % 64 == 0
 
 
+def gemm_res_supported(N: int, K: int, B: int, hw: int) -> bool:
+    """Shapes and row groupings cp25_gemm_res is built for: gemm_supported, and B entries per token dividing the 16
+    rows a lane group's gate lookup spans with at least 16 / B tokens per frame (gemm.hip, gemm_launch)."""
+    return gemm_supported(N, K) and B > 0 and 16 % B == 0 and hw >= 16 // B
+
+
 def gemm_epi(a: torch.Tensor, w: torch.Tensor, epilogue: int = EPI_NONE, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out[M, N] = epi(a[M, K] w[N, K]^T) in bf16 (cp25_gemm_epi); EPI_GELU applies the exact-erf GELU to the
     bf16 product (GPT2FeedForward layer1 + activation)."""

@@ -201,6 +201,9 @@ class MinimalV1LVGDiT:
         self.force_lanes = False  # run the per-batch-entry lanes at CP = 1 too (CP parity tests)
         # optional list collecting (start, end, flop) HIP events around every self-attention launch
         self.attn_events: Optional[list] = None
+        # optional list collecting (start, end) HIP events around every context-parallel K/V gather wait on the compute
+        # stream: the time the stream stood still for the all-gather, i.e. the communication the lanes did not hide
+        self.comm_events: Optional[list] = None
         # "bf16" (the reference's precision) or "fp8": the block projections and MLP as fp8 MFMA GEMMs
         # with row-scaled activations and per-output-channel weight scales (config 5, see set_linear_precision)
         self.linear_precision = "bf16"
@@ -224,9 +227,10 @@ class MinimalV1LVGDiT:
 
     def set_linear_precision(self, precision: str) -> None:
         """"bf16" (default, the reference's arithmetic) or "fp8": the 28 blocks' q/k/v, output, cross-q,
-        cross-output and MLP projections run as hipBLASLt fp8 (OCP E4M3) MFMA GEMMs, activations quantised
-        per row by cp25_quant_fp8_rows (the MLP's fused with its GELU, cp25_gelu_quant_fp8), weights per
-        output channel (once, on first use). Embedders, AdaLN, the text projection and the final layer
+        cross-output and MLP projections run as fp8 (OCP E4M3) MFMA GEMMs, the hand-written cp25_gemm_fp8 (with the
+        gated residual fused into the output projections' epilogue, cp25_gemm_fp8_res; torch._scaled_mm for shapes it
+        is not built for or with block_gemm = "lib"), activations quantised per row by cp25_quant_fp8_rows (the MLP's
+        fused with its GELU, cp25_gelu_quant_fp8), weights per output channel (once, on first use). Embedders, AdaLN, the text projection and the final layer
         stay bf16/fp32. The reference has no fp8 path: the cost is stated against the bf16 path
         (DESIGN.md §4), not pinned to a reference output."""
         if precision not in ("bf16", "fp8"):
@@ -316,6 +320,14 @@ class MinimalV1LVGDiT:
         """The hand-written fp8 GEMM runs this projection (fp8 option): shapes it is built for, block_gemm == "own"."""
         return self.block_gemm == "own" and self.linear_precision == "fp8" and N.gemm_fp8_supported(w.shape[0], w.shape[1])
 
+    def _fused_res(self, a, w: torch.Tensor, B: int, hw: int) -> int:
+        """Which hand-written GEMM carries this projection's gated residual in its epilogue: 1 bf16 (cp25_gemm_res),
+        2 fp8 (cp25_gemm_fp8_res), 0 none (library GEMM, the residual in cp25_ln_mod / the final layer). Both need
+        16 % B == 0 and at least 16 / B tokens per frame (N.gemm_res_supported)."""
+        if not N.gemm_res_supported(w.shape[0], w.shape[1], B, hw):
+            return 0
+        return 1 if self._own(a, w) else (2 if self._own_fp8(w) else 0)
+
     def _proj(self, x, w: torch.Tensor, key: str) -> torch.Tensor:
         """A block projection without epilogue (QKV, cross-attention q)."""
         return N.gemm_epi(x, w) if self._own(x, w) else self._linear(x, w, key)
@@ -328,9 +340,10 @@ class MinimalV1LVGDiT:
         cp25_ln_mod. Returns (x' [n, B, D], h or None)."""
         D = w.shape[0]
         fused = None
-        if self._own(a, w):
+        path = self._fused_res(a, w, B, geo.hw)
+        if path == 1:
             fused = N.gemm_res(a, w, x, x_st, x_sb, gate, B=B, tok0=geo.tok0, hw=geo.hw)
-        elif self._own_fp8(w):
+        elif path == 2:
             q, s = a if isinstance(a, tuple) else N.quant_fp8_rows(a, gelu=gelu_in)
             w8, ws = self._fp8_weight(key, w)
             fused = N.gemm_fp8(q, s, w8, ws, res=(x, x_st, x_sb, gate, B, geo.tok0, geo.hw))
@@ -757,7 +770,7 @@ class MinimalV1LVGDiT:
                 u = self._linear(h1, w1, pre + "mlp.layer1")
                 if self.linear_precision == "bf16":
                     N.gelu_(u)
-            if self._own(u, w2) or self._own_fp8(w2):
+            if self._fused_res(u, w2, B, geo.hw):
                 x, h = self._proj_res(u, w2, pre + "mlp.layer2", x, B * D, D, g_ml, B, geo, n, lnk, sh, sc,
                                       gelu_in=self.linear_precision == "fp8")
                 y, gate_prev = None, None
@@ -817,7 +830,14 @@ class MinimalV1LVGDiT:
         q_scale, attn_kw = self._self_attn_mode(i, hd)
         N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=0, weight=p[pre + "self_attn.q_norm.weight"],
                             cos=cos, sin=sin, out_scale=q_scale)
+        w_ev = None
+        if self.comm_events is not None:
+            w_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            w_ev[0].record()
         work.wait()
+        if w_ev is not None:
+            w_ev[1].record()
+            self.comm_events.append(w_ev)
         kc, vc = kv_chunk_views(kv_all, cp_size * n, B, H, hd)
         attn_kw = self._fp8_qk(qkv[:, :D], kv_all[:, :D], B, H, hd, attn_kw, vc)
         if e0 is not None:

@@ -32,8 +32,11 @@ constexpr int kQRows = 32;     // query rows per wave
 constexpr int kQBlk = kWaves * kQRows;  // 256 query rows per workgroup
 constexpr int kKBlk = 64;      // keys per tile
 constexpr int kThreads = kWaves * 64;
-// Softmax-shift ranges (log2 units). A term is 2^(s - shift); the row sum of up to ~1.4e5 keys of 2^96 stays far inside
-// fp32 (1e34 < 3.4e38, and O = sum P v below it for |v| up to 3e4), bf16 P has the fp32 exponent range.
+// Softmax-shift ranges (log2 units). A term is 2^(s - shift) <= 2^kTop, so a row sum is <= Lk 2^96 and O = sum P v is
+// <= Lk 2^96 max|v|: inside fp32 (2^128) while max|v| Lk < 2^32, e.g. |v| < 2.6e4 at config 4's Lk = 163 800 (the
+// DiT's v is a bf16 projection of a normalised row, orders of magnitude smaller; checked at the top of the window
+// over 163 840 keys with |v| ~ 400 by tests/test_attn_m16_gpu.py::test_m16_zero_shift_top_of_window_long_keys). The
+// contract guard below poisons a row whose sum overflows. bf16 P has the fp32 exponent range.
 constexpr float kTop = 96.f;        // zero / fixed shift: largest exponent a term may reach
 constexpr float kMaxBound = 98.f;   // fixed shift: largest score bound b (smallest row-max term 2^(96 - 2 b) >= 2^-100)
 constexpr float kTopF8 = 60.f;      // fp8 Q K^T form: P = exp2(S) unshifted for bound products up to this
@@ -320,6 +323,47 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
   };
   char* const k_wr = smem + srow * kKStride16 + sch * 16;
   char* const v_wr = smem + VB0 + srow * kVStride16 + sch * 16;
+
+  // LDS-DMA staging (per-block kernels): K tiles always (group B), V tiles too in the online form (group A), straight
+  // into the padded 288-B rows, so the readers keep their immediate offsets and no staging VGPRs are live. The register
+  // path cost 4.7 % of the launch in load issue and register-file return (profiles/r3/attn_nop/staging_load_probe.log);
+  // by DMA: zero shift -1.95 %, online max -3.2 % (K and V; K alone spills in the online form, V by DMA in the zero-
+  // shift form measured slower), profiles/r3/attn_nop/dma_staging_ab.log. Instruction j of a group's wave wb moves tile
+  // bytes [1024 (wb + 4 j), +1024) of the 64 x 288-B image (18 per tile: waves 0-1 issue 5, waves 2-3 issue 4); lane l
+  // the 16 B at byte 16 l of it: row bb / 288, column bb % 288 (columns >= 256 are the row padding and re-read the
+  // tile's first 16 B). Rows past Lk on the ragged tile re-read row rows - 1: finite, and their scores are masked to
+  // -inf (K) or multiplied by P = 0 (V). The persistent form keeps the register path (its Q copy owns the DMA waits).
+  constexpr bool kDmaK = !kPersist;
+  constexpr bool kDmaV = kDmaK && online;
+  const int wb = wave_u & 3;  // wave within its group
+  int dma_off[5];             // lane source offsets of a full tile, per instruction
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int bb = 1024 * (wb + 4 * j) + 16 * lane;
+    const int row = bb / kKStride16, cb = bb - row * kKStride16;
+    dma_off[j] = cb < 2 * kD ? row * (int)(sl * 2) + cb : 0;
+  }
+  auto dma_tile = [&](int t, auto BUF) __attribute__((always_inline)) {  // group B: K(t), group A: V(t)
+    constexpr int kb = decltype(BUF)::value ? KB1 : 0;
+    const char* tsrc = sbase + (int64_t)t * kKBlk * sl * 2;
+    const int rows = min(Lk - t * kKBlk, kKBlk);
+    if (rows <= 0) return;  // no such tile (wave-uniform; callers stage only existing tiles)
+    const unsigned lds0 = (unsigned)(uintptr_t)(lds_char_ptr)(smem + (group_b ? kb : VB0 + (kb ? kVBuf16 : 0)));
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      if (wb + 4 * j >= 18) break;  // wave-uniform
+      int off = dma_off[j];
+      if (__builtin_expect(rows < kKBlk, 0)) {
+        const int bb = 1024 * (wb + 4 * j) + 16 * lane;
+        const int row = bb / kKStride16, cb = bb - row * kKStride16;
+        off = cb < 2 * kD ? min(row, rows - 1) * (int)(sl * 2) + cb : 0;
+      }
+      // inline asm (as dma_q): a compiler-visible LDS-DMA makes the compiler drain vmcnt before every s_barrier.
+      // M0 is reserved (never allocated); the s_nop 0 separates its write from the DMA that reads it.
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(tsrc),
+                   "s"(lds0 + 1024 * (wb + 4 * j)) : "memory");
+    }
+  };
   auto write_k = [&](auto BUF) __attribute__((always_inline)) {
     constexpr int kb = decltype(BUF)::value ? KB1 : 0;
 #pragma unroll
@@ -551,14 +595,24 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
   typedef std::integral_constant<int, 1> B1;
 
   // ---- prologue: K(0), V(0) -> buffer 0; K(1) -> buffer 1; S(0) for everyone, P(0) for A ----
-  load_tile(0);
-  if (group_b) write_k(B0{}); else write_v(B0{});
-  if (group_b) {
-    load_tile(1);
-    write_k(B1{});
-    load_tile(2);  // written in phase 0
+  if (kDmaK && group_b) {
+    // only tiles that exist: past the last one the row clamp would go negative (the DMA's VGPR offset is unsigned)
+    dma_tile(0, B0{});
+    if (ntiles > 1) dma_tile(1, B1{});
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else if (kDmaV) {
+    dma_tile(0, B0{});  // V(0)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else {
-    load_tile(1);  // written in phase 1
+    load_tile(0);
+    if (group_b) write_k(B0{}); else write_v(B0{});
+    if (group_b) {
+      load_tile(1);
+      write_k(B1{});
+      load_tile(2);  // written in phase 0
+    } else {
+      load_tile(1);  // written in phase 1
+    }
   }
   __syncthreads();
   qk_mma(B0{});
@@ -644,10 +698,16 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
       mfma_phase(PAR, std::false_type{});
       __syncthreads();
       if (t + 1 < ntiles) {
-        write_v(std::integral_constant<int, par ^ 1>{});  // drains under the softmax VALU
-        softmax(t + 1);
-        load_tile(t + 2);
+        if constexpr (kDmaV) {
+          dma_tile(t + 1, std::integral_constant<int, par ^ 1>{});  // V(t+1): its buffer is free since the last barrier
+          softmax(t + 1);
+        } else {
+          write_v(std::integral_constant<int, par ^ 1>{});  // drains under the softmax VALU
+          softmax(t + 1);
+          load_tile(t + 2);
+        }
       }
+      if constexpr (kDmaV) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // V(t+1) landed before the next P.V
       __syncthreads();
     };
     // pairs of tiles (constexpr buffer parity), then the odd last tile: one loop exit
@@ -659,9 +719,15 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
   } else {
     // group B: phase 2t softmax(t) + K(t+2) staging, phase 2t+1 MFMA
     auto step = [&](auto PAR, int t) __attribute__((always_inline)) {
-      if (t + 2 < ntiles) write_k(PAR);
+      if constexpr (kDmaK) {
+        if (t + 2 < ntiles) dma_tile(t + 2, PAR);  // buffer t & 1: K(t) was consumed in the last two phases
+      } else {
+        if (t + 2 < ntiles) write_k(PAR);
+      }
       softmax(t);
-      if (t + 2 < ntiles) load_tile(t + 3);
+      if constexpr (!kDmaK) {
+        if (t + 2 < ntiles) load_tile(t + 3);
+      }
       static_for<kAhead>([&](auto NC) __attribute__((always_inline)) { issue_pair(PAR, NC); });
       // a raw barrier behind a counted wait: the K(t+2) writes retire, the kAhead pairs' reads just issued stay in
       // flight across it (a __syncthreads() fence waited for them too, before the barrier, on the longer phase)
@@ -669,6 +735,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       mfma_phase(PAR, std::true_type{});
+      if constexpr (kDmaK) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K(t+2) landed before A reads it
       __syncthreads();
     };
     for (int t = 0; t + 1 < ntiles; t += 2) {

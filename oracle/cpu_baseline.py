@@ -11,9 +11,15 @@ extrapolated (BASELINE.md "CPU-baseline plan"):
     scaled by L / n_q;
   * one forward = 28 blocks; one video = 72 forwards (36 Karras evaluations x CFG 2). The VAE
     (~0.5 % of the FLOPs) is not included.
+The query slice is processed in chunks of 1 024 queries (the fp32 score matrix of one chunk is 7 GB at L = 109 120).
+config1_end_to_end() times BASELINE config 1 whole on the CPU: the oracle's Image2World at
+256 x 256 x 9 frames, 2 Karras UniPC steps (3 evaluations x CFG 2) of the 2B net, VAE encode of the conditioning
+frame and decode of the 3 latent frames.
 """
 from __future__ import annotations
 
+import dataclasses
+import os
 import time
 
 import torch
@@ -26,7 +32,18 @@ def _rms(x, eps=1e-6):
     return x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + eps)
 
 
-def dit_block_sample(L: int = 109120, D: int = 2048, H: int = 16, n_q: int = 1024, ctx_len: int = 512,
+def host_threads(requested: int | None = None) -> tuple[int, int]:
+    """(threads to use, host cores visible to this process): the affinity mask's size, capped by OMP_NUM_THREADS (the
+    GPU box's CPU share: its affinity shows the whole machine) and by an explicit request."""
+    visible = len(os.sched_getaffinity(0))
+    cap = int(os.environ.get("OMP_NUM_THREADS", visible) or visible)
+    n = min(visible, cap)
+    if requested:
+        n = min(n, requested)
+    return max(1, n), visible
+
+
+def dit_block_sample(L: int = 109120, D: int = 2048, H: int = 16, n_q: int = 4096, ctx_len: int = 512,
                      n_blocks: int = 28, forwards: int = 72, frames: int = 121, threads: int | None = None,
                      seed: int = 0) -> dict:
     if threads is not None:
@@ -55,13 +72,17 @@ def dit_block_sample(L: int = 109120, D: int = 2048, H: int = 16, n_q: int = 102
     v = (h @ Wv.t()).view(L, H, hd)
     t_full = time.perf_counter() - t0
 
-    # ---- per-query slice
+    # ---- per-query slice (the attention in chunks of 1 024 queries)
     t0 = time.perf_counter()
     hq = h[:n_q]
     q = _rms((hq @ Wq.t()).view(n_q, H, hd))
     q = apply_rope(q[None], freqs[:n_q])[0]
-    att = torch.softmax(torch.einsum("qhd,khd->hqk", q, k) * hd ** -0.5, -1)
-    o = torch.einsum("hqk,khd->qhd", att, v).reshape(n_q, D) @ Wo.t()
+    o = torch.empty(n_q, H, hd)
+    for c0 in range(0, n_q, 1024):
+        att = torch.softmax(torch.einsum("qhd,khd->hqk", q[c0:c0 + 1024], k) * hd ** -0.5, -1)
+        o[c0:c0 + 1024] = torch.einsum("hqk,khd->qhd", att, v)
+        del att
+    o = o.reshape(n_q, D) @ Wo.t()
     xs = x[:n_q] + gate * o
     h2 = F.layer_norm(xs, (D,), eps=1e-6) * (1 + scale) + shift
     qc = _rms((h2 @ Wqc.t()).view(n_q, H, hd))
@@ -83,6 +104,43 @@ def dit_block_sample(L: int = 109120, D: int = 2048, H: int = 16, n_q: int = 102
         "block_seconds_extrapolated": block_s,
         "sample_seconds": t_full + t_slice,
         "sample": (f"oracle fp32 PyTorch-CPU restatement of one 2B DiT block at L={L} (720p x 121f): LN + K/V "
-                   f"projections over all tokens, a {n_q}-query slice of everything else, extrapolated x L/{n_q} "
-                   f"x {n_blocks} blocks x {forwards} forwards; VAE excluded"),
+                   f"projections over all tokens, a {n_q}-query slice ({100.0 * n_q / L:.2f} % of the queries) of "
+                   f"everything else, extrapolated x L/{n_q} x {n_blocks} blocks x {forwards} forwards; VAE excluded"),
     }
+
+
+def config1_end_to_end(threads: int | None = None, seed: int = 0) -> dict:
+    """BASELINE config 1 on the CPU, whole: the oracle's Image2World video at 256 x 256 x 9 frames (latent
+    [16, 3, 32, 32]), 2 Karras UniPC steps with CFG (guidance 7, zeroed uncond context) of the seeded 2B net, the VAE
+    encode of the conditioning frame and the decode of all 9 frames (bf16 activations as the reference runs them).
+    Weight construction is not timed."""
+    from cosmos_predict2.dit import init_state_dict  # seeded weights with the 2B shapes (the bench's own init)
+    from cosmos_predict2.net_config import DIT_2B
+    from cosmos_predict2.vae import init_vae_state_dict
+
+    from . import sampler as osamp
+    from . import vae as ovae
+
+    if threads is not None:
+        torch.set_num_threads(threads)
+    sd = {"net." + k: v for k, v in init_state_dict(DIT_2B, seed=11, zero_adaln_out=False).items()}
+    vsd = init_vae_state_dict(seed=0)
+    g = torch.Generator().manual_seed(seed)
+    img = torch.rand(1, 3, 1, 256, 256, generator=g) * 2 - 1
+    ctx_c = torch.randn(1, 512, DIT_2B.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
+    ctx_u = torch.zeros_like(ctx_c)
+    t0 = time.perf_counter()
+    lat0 = ovae.encode(vsd, img)  # [1, 16, 1, 32, 32]
+    gt = torch.zeros(1, 16, 3, 32, 32)
+    gt[:, :, :1] = lat0.float()
+    t1 = time.perf_counter()
+    lat = osamp.generate(dataclasses.asdict(DIT_2B), sd, gt, ctx_c, ctx_u, num_cond=1, guidance=7.0, seed=0,
+                         num_steps=2, use_karras=True, cond_frame_t=0.1)
+    t2 = time.perf_counter()
+    video = ovae.decode(vsd, lat)
+    t3 = time.perf_counter()
+    assert video.shape[2] == 9 and torch.isfinite(video.float()).all()
+    return {"frames_per_s": 9 / (t3 - t0), "seconds": t3 - t0, "encode_s": t1 - t0, "sampler_s": t2 - t1,
+            "decode_s": t3 - t2, "cores": torch.get_num_threads(),
+            "sample": "BASELINE config 1 whole on the CPU: oracle Image2World 256x256x9f, 2B net, 2 Karras UniPC steps "
+                      "(3 evals x CFG 2), VAE encode of the conditioning frame + decode of 9 frames"}

@@ -199,3 +199,23 @@ def test_m16_full_metric_shape_query_slice(device):
         torch.cuda.synchronize()
         assert ((oc.float() - 0.75).abs() <= 0.75 * 2 ** -7).all()
         del o, oc, qs, k, v
+
+
+def test_m16_zero_shift_top_of_window_long_keys(device):
+    """The zero-shift window's headroom (attn_fwd.hip kTop = 96): every score of every row at the top of the window
+    (q and k aligned, 95.9 log2 units) over 163 840 keys (> config 4's 163 800), |v| up to ~400: the row sum reaches
+    2^113.2 and O ~2^122, inside fp32 (the window holds while |v| Lk < 2^32). All terms equal, so O = mean(v) exactly
+    up to the bf16 output rounding."""
+    Lq, Lk = 256, 163840
+    g = torch.Generator(device="cpu").manual_seed(13)
+    q = torch.zeros(1, Lq, 1, 128)
+    k = torch.zeros(1, Lk, 1, 128)
+    q[..., 0], k[..., 0] = 8.0, 11.984375  # bf16-exact; pre-scaled score 95.875 (log2 units)
+    v = (torch.randn(1, Lk, 1, 128, generator=g) * 100.0).to(device, torch.bfloat16)
+    q, k = q.to(device, torch.bfloat16), k.to(device, torch.bfloat16)
+    assert N.attn_kernel_name(Lk, None, (8.0, 12.0), True).endswith("zero shift>")
+    o = N.attn_fwd(q, k, v, norm_bounds=(8.0, 12.0), prescaled=True)
+    torch.cuda.synchronize()
+    assert torch.isfinite(o.float()).all()
+    mean_v = v.float().mean(1)[0, 0]
+    assert rel_l2(o[0, :, 0], mean_v.expand(Lq, 128)) <= 2 ** -8

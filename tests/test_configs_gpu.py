@@ -4,8 +4,9 @@
   gathered keys, 40 heads of 128, the CFG pair batched (B = 2); checked on a query slice (first and
   last rows, the last query block ragged) against fp32 math, with the library's split plan and the
   bounded-shift softmax the DiT uses.
-* Config 4 (2B multiview, 7 views x 480p x 57 frames): joint self-attention over 7 x 15 x 27 x 48 =
-  136 080 tokens (B = 2, 16 heads), query slice vs fp32.
+* Config 4 (2B multiview, 7 views x 480p x 57 frames; multiview's 480p is 480 x 832): joint self-attention over
+  7 x 15 x 30 x 52 = 163 800 tokens (B = 2, 16 heads; ragged last key tile and query block), query slice vs fp32, in
+  the DiT's prescaled form too.
 * Config 5 (2B action-conditioned, fp8 block GEMMs): one full-depth (28-block) forward of the
   action net on a 13-frame 480 x 640 chunk (4 latent frames x 30 x 40 = 4 800 tokens) vs the bf16
   oracle, bf16 path and fp8 path; the reference has no fp8 path, so the fp8 bound is a stated
@@ -54,16 +55,31 @@ def test_config3_14b_cp8_rank_attention(device):
     assert err <= 4e-3, err
 
 
-def test_config4_multiview_joint_attention(device):
-    B, H, L = 2, 16, 7 * 15 * 27 * 48
+@pytest.mark.parametrize("form", ["bounded", "prescaled", "online"])
+def test_config4_multiview_joint_attention(device, form):
+    B, H, L = 2, 16, 7 * 15 * 30 * 52
+    assert L == 163800
     q = _normed((B, L, H, 128), 4, device)
     k = _normed((B, L, H, 128), 5, device)
     v = torch.randn((B, L, H, 128), device=device, generator=torch.Generator(device=device).manual_seed(6)).to(BF16)
     nb = (128 ** 0.5 * 1.02, 128 ** 0.5 * 1.02)
-    out = N.attn_fwd(q, k, v, norm_bounds=nb)
-    rows = torch.cat([torch.arange(0, 16), torch.arange(L // 2, L // 2 + 16), torch.arange(L - 32, L)]).to(device)
-    err = _slice_check(q, k, v, out, rows)
-    print(f"config 4 joint 7-view attention (L {L}): rel-L2 {err:.2e}")
+    if form == "bounded":
+        out = N.attn_fwd(q, k, v, norm_bounds=nb)
+    else:
+        # the DiT's form: q carries scale * log2(e) (rounded once); "online": bounds past every fixed window
+        c = 128 ** -0.5 * 1.4426950408889634
+        qc = (q.float() * c).to(BF16)
+        bounds = (nb[0] * c, nb[1]) if form == "prescaled" else (nb[0] * c * 8, nb[1])
+        out = N.attn_fwd(qc, k, v, norm_bounds=bounds, prescaled=True)
+        q = qc
+    rows = torch.cat([torch.arange(0, 16), torch.arange(L // 2, L // 2 + 16), torch.arange(L - 40, L)]).to(device)
+    qs = q[:, rows].float()
+    # prescaled scores are in log2 units: x ln 2 back to natural ones
+    s = torch.einsum("bqhd,bkhd->bhqk", qs, k.float()) * (0.6931471805599453 if form != "bounded" else 128 ** -0.5)
+    ref = torch.einsum("bhqk,bkhd->bqhd", torch.softmax(s, -1), v.float())
+    err = ((out[:, rows].float() - ref).norm() / ref.norm()).item()
+    print(f"config 4 joint 7-view attention (L {L}, {form}, kernel {N.attn_kernel_name(L, None, bounds if form != 'bounded' else nb, form != 'bounded', 0)}): rel-L2 {err:.2e}")
+    assert torch.isfinite(out).all()
     assert err <= 4e-3, err
 
 

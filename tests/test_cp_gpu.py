@@ -15,6 +15,11 @@ match the single-rank run (guidance 0, 2 Karras steps = 3 evals x CFG).
   quantises exactly as the whole sequence does and CP = 2 must again match CP = 1 bit for bit; the
   fp8 attention too (q / k scales are fixed powers of two, V's per-head scale is taken over the gathered
   keys, which every rank holds whole).
+* trained-size q/k norm weights (uniform in [0.5, 3], bound product ~147): CP > 1 runs the online-max attention on the
+  weight bounds; CP = 1 by default runs the gated pair (data_tight_k_bound: zero shift for every 256-query block whose
+  measured bound allows it, chosen per block of the whole sequence, the max |k| taken over the whole CFG batch), so
+  the two round P at different shifts: bit-identity holds against CP = 1 with data_tight_k_bound = False ("nw_weight"),
+  and against the default CP = 1 the distance is rounding ("nw_gated", <= 1.5e-2 like the split plan's).
 """
 import os
 import socket
@@ -38,12 +43,17 @@ def _port():
     return p
 
 
-def _case():
+def _case(norm_weights=False):
     from cosmos_predict2.dit import init_state_dict
     from cosmos_predict2.net_config import SamplerConfig, tiny_dit
 
     cfg = tiny_dit(num_blocks=2)
     sd = {"net." + k: v for k, v in init_state_dict(cfg, seed=3, zero_adaln_out=False).items()}
+    if norm_weights:  # trained-checkpoint scale: past the zero/fixed-shift windows
+        gw = torch.Generator().manual_seed(9)
+        for k in sd:
+            if k.endswith(("q_norm.weight", "k_norm.weight")):
+                sd[k] = (0.5 + 2.5 * torch.rand(sd[k].shape, generator=gw)).to(torch.bfloat16)
     g = torch.Generator().manual_seed(30)
     # 768 tokens: 384 per rank and lane, so every GEMM has M >= 384 (hipBLASLt picks a different,
     # differently-rounding kernel for the MLP's K = 2048 GEMM at M = 192: tools/diag_gemm_m.py)
@@ -61,6 +71,8 @@ def _run(model, gt, cc, cu, shape, dev):
 
 
 def _set_precision(m, precision):
+    if precision.startswith("nw_"):
+        return
     if precision == "fp8attn":
         m.net.set_attention_precision("fp8")
     else:
@@ -75,7 +87,7 @@ def _worker(rank, world, port, q, split_env, precision="bf16"):
         from cosmos_predict2.model import Video2WorldModelRectifiedFlow
 
         dev = torch.device("cuda:0")
-        cfg, scfg, sd, gt, cc, cu, shape = _case()
+        cfg, scfg, sd, gt, cc, cu, shape = _case(precision.startswith("nw_"))
         m = Video2WorldModelRectifiedFlow(cfg, scfg, device=dev)
         m.load_state_dict(sd)
         _set_precision(m, precision)
@@ -88,7 +100,8 @@ def _worker(rank, world, port, q, split_env, precision="bf16"):
 
 @pytest.mark.parametrize("world,split_env,tol,precision", [(2, "1", 0.0, "bf16"), (2, "", 1.5e-2, "bf16"),
                                                            (2, "1", 0.0, "fp8"), (2, "1", 0.0, "fp8attn"),
-                                                           (4, "1", 0.0, "bf16")])
+                                                           (4, "1", 0.0, "bf16"), (2, "1", 0.0, "nw_weight"),
+                                                           (2, "1", 1.5e-2, "nw_gated")])
 def test_cp2_matches_cp1(device, monkeypatch, world, split_env, tol, precision):
     """world ranks over gloo sharing cuda:0: the real dit.forward_tokens lanes, each K/V all-gather a deferred gloo
     work (context_parallel._GlooDeferred: the gathered rows land only at the lane's wait(), after the other lane's
@@ -99,11 +112,15 @@ def test_cp2_matches_cp1(device, monkeypatch, world, split_env, tol, precision):
         monkeypatch.setattr(N, "_ATTN_SPLIT", int(split_env))
     else:
         monkeypatch.setattr(N, "_ATTN_SPLIT", None)
-    cfg, scfg, sd, gt, cc, cu, shape = _case()
+    cfg, scfg, sd, gt, cc, cu, shape = _case(precision.startswith("nw_"))
     m = Video2WorldModelRectifiedFlow(cfg, scfg, device=device)
     m.load_state_dict(sd)
     _set_precision(m, precision)
     m.net.force_lanes = bool(split_env)
+    if precision.startswith("nw_"):
+        kern = m.net.attention_kernels(shape[1] * shape[2] * shape[3] // 4)
+        assert "gated" in kern["self"], kern  # CP = 1's default with these weights
+        m.net.data_tight_k_bound = precision == "nw_gated"  # nw_weight: the CP path's own (weight-bound) mode
     ref = _run(m, gt, cc, cu, shape, device)
     del m
     torch.cuda.empty_cache()

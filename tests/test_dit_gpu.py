@@ -52,10 +52,9 @@ def test_dit_forward_matches_oracle(device, T, H, W, blocks):
     assert err <= 1e-2, err
 
 
-def _sampler_case(device, guidance):
+def _sampler_case(device, guidance, T=3, H=16, W=16):
     cfg = tiny_dit(num_blocks=2)
     sd, sd_ref = _setup(cfg, seed=1)
-    T, H, W = 3, 16, 16
     g = torch.Generator().manual_seed(20)
     gt = torch.randn(1, 16, T, H, W, generator=g)
     ctx_c = torch.randn(1, 512, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
@@ -76,10 +75,12 @@ def _fake(xv, tv, b):
     return torch.sin(xv.float() * (1.0 + 0.25 * b) + tv)
 
 
+@pytest.mark.parametrize("ncond", [0, 1, 2])
 @pytest.mark.parametrize("num_steps,karras,cft", [(2, True, 0.1), (6, False, -1.0)])
-def test_sampler_plumbing_bit_exact(device, num_steps, karras, cft):
+def test_sampler_plumbing_bit_exact(device, num_steps, karras, cft, ncond):
     """Oracle loop vs fused CFG-batched loop with an identical fake denoiser: patchify, per-frame
-    timesteps, frame replacement, GT velocity, CFG and UniPC must agree bit for bit."""
+    timesteps, frame replacement, GT velocity, CFG and UniPC must agree bit for bit. ncond: the conditional
+    latent frames of Text2World (0), Image2World (1) and Video2World (2) (cosmos_predict2/config.py:459-469)."""
     cfg = tiny_dit()
     T, H, W = 3, 8, 12
     g = torch.Generator().manual_seed(21)
@@ -92,7 +93,7 @@ def test_sampler_plumbing_bit_exact(device, num_steps, karras, cft):
         ts = (t.float() * cfg.timestep_scale)[0]  # [T]
         return _fake(x, ts[None, None, :, None, None], b)
 
-    ref = osamp.generate(dataclasses.asdict(cfg), None, gt, ctx_c, ctx_u, num_cond=1, guidance=7.0, seed=3,
+    ref = osamp.generate(dataclasses.asdict(cfg), None, gt, ctx_c, ctx_u, num_cond=ncond, guidance=7.0, seed=3,
                          num_steps=num_steps, use_karras=karras, cond_frame_t=cft, dit_fn=oracle_fn)
 
     def device_fn(rows, t_B_T, geo):
@@ -103,8 +104,8 @@ def test_sampler_plumbing_bit_exact(device, num_steps, karras, cft):
 
     model = Video2WorldModelRectifiedFlow(cfg, SamplerConfig(use_kerras_sigma_at_inference=karras,
                                                              conditional_frame_timestep=cft), device=device)
-    out = model.sample_latents(gt.to(device), ctx_c, ctx_u, state_shape=(16, T, H, W), num_conditional_frames=1,
-                               guidance=7.0, seed=3, num_steps=num_steps, net_fn=device_fn)
+    out = model.sample_latents(gt.to(device) if ncond else None, ctx_c, ctx_u, state_shape=(16, T, H, W),
+                               num_conditional_frames=ncond, guidance=7.0, seed=3, num_steps=num_steps, net_fn=device_fn)
     assert torch.equal(out.cpu(), ref)
 
 
@@ -117,6 +118,19 @@ def test_sampler_matches_oracle(device, guidance, tol):
     err = _sampler_case(device, guidance)
     print(f"sampler vs oracle (Karras 2 steps = 3 evals x CFG, g={guidance}) rel-L2: {err:.3e}")
     assert err <= tol, err
+
+
+def test_sampler_small_frames_library_residual(device):
+    """A 4 x 6 latent (hw = 2 x 3 = 6 tokens per frame): the fused gated-residual GEMM needs at least 16 / B tokens per
+    frame (gemm_res_supported: 16 at the CFG-shared block 0's B = 1, 8 at B = 2), so every residual projection takes
+    the library GEMM with the residual in cp25_ln_mod / the final layer instead of raising. Same oracle bound as the
+    16 x 16 case."""
+    from cosmos_predict2 import _native as N
+
+    assert not N.gemm_res_supported(512, 512, 1, 6) and not N.gemm_res_supported(512, 512, 2, 6)
+    err = _sampler_case(device, 0.0, T=3, H=4, W=6)
+    print(f"sampler vs oracle at a 4 x 6 latent (library residual path): {err:.3e}")
+    assert err <= 1e-2, err
 
 
 @pytest.mark.parametrize("per_frame", [4, 0])

@@ -62,3 +62,28 @@ def test_race_check_follows_control_flow():
     by no path with the read in flight (no race there: the checker's linear form reported one)."""
     r = isa_check.analyse(_SYNTH, "_Zk")
     assert r["races"] == ["v_add_f32_e32 v22, v2, v23", "v_mov_b32_e32 v3, v24"]
+
+
+_SYNTH2 = """_Zm:
+\tds_read_b128 v[4:7], v10
+\tds_read_b64 a[0:1], v11
+\tv_add_f32_e64 v20, -v5, |v21|
+\tv_mov_b32_e32 v22, a1
+\tds_read_b32 v30, v6 offset:16
+\ts_mov_b32 m0, s2
+\ts_nop 0
+\tglobal_load_lds_dwordx4 v31, s[4:5]
+\ts_waitcnt lgkmcnt(0)
+\tv_mov_b32_e32 v23, v4
+\ts_endpgm
+.Lfunc_end1:
+"""
+
+
+def test_race_check_sees_modifiers_agprs_and_addresses():
+    """A register behind a source modifier (-v5), an AGPR destination (a1) and a ds_read whose ADDRESS is still in
+    flight (v6) are each a race; the s_nop 0 after an M0 write (the LDS-DMA asm's own) is not counted as a hazard pad;
+    after lgkmcnt(0) nothing is in flight."""
+    r = isa_check.analyse(_SYNTH2, "_Zm")
+    assert r["races"] == ["v_add_f32_e64 v20, -v5, |v21|", "v_mov_b32_e32 v22, a1", "ds_read_b32 v30, v6 offset:16"]
+    assert r["nops"] == 0 and r["m0_nops"] == 1
