@@ -108,8 +108,10 @@ def apply_rope(x: torch.Tensor, freqs: torch.Tensor) -> torch.Tensor:
 
 
 def sdpa(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, chunk: int = 4096) -> torch.Tensor:
-    """[B, S, H, D] bf16 -> [B, S, H*D] bf16 with fp32 softmax (query-chunked for memory)."""
+    """[B, S, H, D] bf16 -> [B, S, H*D] bf16 with fp32 softmax (query-chunked for memory: a chunk's fp32 scores stay
+    under ~16 GB, e.g. 384 queries at config 4's 163 800 keys)."""
     B, Lq, H, D = q.shape
+    chunk = max(128, min(chunk, (16 << 30) // (B * H * k.shape[1] * 4) // 128 * 128))
     kf = k.float().transpose(1, 2)
     vf = v.float().transpose(1, 2)
     outs = []

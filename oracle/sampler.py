@@ -56,15 +56,17 @@ def generate(cfg_dit: dict, sd: dict, gt: torch.Tensor, ctx_cond: torch.Tensor, 
              num_cond: int, guidance: float, seed: int, num_steps: int, shift: float = 5.0,
              use_karras: bool = False, cond_frame_t: float = -1.0, return_trajectory: bool = False,
              dit_fn=None):
-    """generate_samples_from_batch for Video2World with CFG. gt: x0 latent [1, C, T, H, W] fp32."""
+    """generate_samples_from_batch for Video2World with CFG. gt: x0 latent [1, C, T, H, W] fp32. Runs on gt's device
+    (the large-config tests run it on the GPU's own torch ops; the noise is drawn on the host as the reference does)."""
     B, C, T, H, W = gt.shape
-    noise = arch_invariant_rand((B, C, T, H, W), seed)
+    dev = gt.device
+    noise = arch_invariant_rand((B, C, T, H, W), seed).to(dev)
     sched = UniPC(num_steps, shift=shift, use_karras=use_karras)
-    mask = frame_mask(B, T, H, W, num_cond, dtype=gt.dtype)
+    mask = frame_mask(B, T, H, W, num_cond, dtype=gt.dtype).to(dev)
     x = noise
     traj = []
     for t in sched.timesteps:
-        t_B_T = torch.stack([t]).unsqueeze(0)  # [1, 1] int64
+        t_B_T = torch.stack([t]).unsqueeze(0).to(dev)  # [1, 1] int64
         vc = denoise(cfg_dit, sd, noise, x, t_B_T, ctx_cond, gt, mask, cond_frame_t, dit_fn=dit_fn)
         vu = denoise(cfg_dit, sd, noise, x, t_B_T, ctx_uncond, gt, mask, cond_frame_t, dit_fn=dit_fn)
         v = vc + guidance * (vc - vu)
