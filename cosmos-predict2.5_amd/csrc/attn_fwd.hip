@@ -15,7 +15,7 @@
 //   attn_fwd_f8   the config-5 fp8 option (no reference counterpart): Q K^T on v_mfma_f32_32x32x64_f8f6f4 over e4m3
 //                 q / k, and with kF8 = 3 also P.V on e5m2 P (made without exp2) and e4m3 V^T tiles.
 // Archived variants and A/B switches of round 2 (one wave per SIMD, LDS-DMA staging, V^T tiles, persistent
-// cross-attention, 32x32x16 bf16 forms, lab isolation builds): tools/lab/attn_fwd_r2.hip.
+// cross-attention, 32x32x16 bf16 forms, lab isolation builds): git show caf7e63:tools/lab/attn_fwd_r2.hip (tools/lab/README.md).
 // NaN inputs are not supported (built with -fno-honor-nans; the reference's flash kernels do not define NaN
 // propagation either). Numerics: scores, shifts and sums fp32, P rounded to bf16 before P.V (as every flash kernel
 // the reference dispatches to does), O accumulated in fp32, normalised and rounded once to bf16.

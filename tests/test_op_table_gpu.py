@@ -97,13 +97,14 @@ def test_head_rmsnorm_rope(device):
     record("q/k RMSNorm + RoPE (cp25_head_rmsnorm_rope)", hip, ref, truth, 2e-3)
 
 
-def _qkv(B, L, Lk, H, g, dev, wq=1.0):
+def _qkv(B, L, Lk, H, g, dev, wq=1.0, q_fp32=False):
     q = torch.randn(B, L, H, 128, generator=g, device=dev)
     k = torch.randn(B, Lk, H, 128, generator=g, device=dev)
-    q = (q * torch.rsqrt(q.pow(2).mean(-1, keepdim=True)) * wq).to(BF16)
+    q32 = q * torch.rsqrt(q.pow(2).mean(-1, keepdim=True)) * wq  # the q RMSNorm's fp32 result before its bf16 rounding
+    q = q32.to(BF16)
     k = (k * torch.rsqrt(k.pow(2).mean(-1, keepdim=True))).to(BF16)
     v = torch.randn(B, Lk, H, 128, generator=g, device=dev).to(BF16)
-    return q, k, v
+    return (q, k, v, q32) if q_fp32 else (q, k, v)
 
 
 def _attn_truth(q, k, v, qf=None):
@@ -115,18 +116,22 @@ def _attn_truth(q, k, v, qf=None):
 @pytest.mark.parametrize("Lk", [4096, 512])
 def test_attention(device, Lk):
     """cp25_attn_fwd_* (networks/attention.py:90-181): both the form with q rounded where the reference rounds it
-    (bounded) and the DiT's default (q * scale * log2 e rounded once, prescaled)."""
+    (bounded) and the DiT's default (q * scale * log2 e rounded once, prescaled). The truth keeps q in fp32 (the q
+    RMSNorm's result before any rounding): the reference rounds it to bf16 once, the DiT's prescaled form rounds q * c
+    once (its RMSNorm/RoPE kernel emits bf16(q c) from fp32), so each path carries exactly one q rounding. (Rounding an
+    already bf16 q times c again -- bf16(bf16(q) c), as this test did until round 4 -- adds a second rounding and read
+    as a 21 % parity cost of the prescaled form that the DiT does not have: tests/test_prescaled_q_cpu.py.)"""
     B, L, H = 1, 4096, 4
     g = torch.Generator(device=device).manual_seed(3 + Lk)
-    q, k, v = _qkv(B, L, Lk, H, g, device)
+    q, k, v, q32 = _qkv(B, L, Lk, H, g, device, q_fp32=True)
     ref = odit.sdpa(q, k, v).view(B, L, H, 128)
-    truth = _attn_truth(q, k, v)
+    truth = _attn_truth(q, k, v, qf=q32)
     bounds = (q.float().norm(dim=-1).max().item() * 1.01, k.float().norm(dim=-1).max().item() * 1.01)
     kind = "self" if Lk > 512 else "cross (Lk 512)"
     hip = N.attn_fwd(q, k, v, norm_bounds=bounds)
     record(f"{kind}-attention, q rounded as the reference (cp25_attn_fwd_bounded)", hip, ref, truth, 4e-3)
     c = 128 ** -0.5 * math.log2(math.e)
-    qs = (q.float() * c).to(BF16)
+    qs = (q32 * c).to(BF16)
     hip_p = N.attn_fwd(qs, k, v, prescaled=True, norm_bounds=(bounds[0] * c * 1.01, bounds[1]))
     record(f"{kind}-attention, DiT default: q*c rounded once (cp25_attn_fwd_prescaled)", hip_p, ref, truth, 4e-3)
 

@@ -1,8 +1,8 @@
 #!/bin/bash
 # Lab builds of libcp25.so with extra attn_fwd.hip defines, for same-box A/B runs of
 # tools/bench_attn.py --lib tools/lab/libcp25_<name>.so (not part of the product build).
-# usage: [SRC=tools/lab/attn_fwd_r2.hip] tools/lab/build.sh <name> [-DFOO ...]  (SRC: the attention source; default
-# the product attn_fwd.hip; tools/lab/attn_fwd_r2.hip holds the round-2 variants and lab switches)
+# usage: [SRC=/tmp/x.hip] tools/lab/build.sh <name> [-DFOO ...]  (SRC: the attention source; default the product
+# attn_fwd.hip; a generated variant or an earlier build from git history, tools/lab/README.md)
 set -e
 cd "$(dirname "$0")/../.."
 make -C cosmos-predict2.5_amd/csrc -j8 >/dev/null
