@@ -116,7 +116,52 @@ def gelu_(x):
     return x
 
 
-_FUNCS = dict(ln_mod=ln_mod, final_ln_mod=final_ln_mod, head_rmsnorm_rope=head_rmsnorm_rope, copy_rows=copy_rows,
+# ---- VAE entry points (the banded decode's host path on the CPU). Computed in float64 and rounded once to bf16, so an
+# output pixel does not depend on how much of the image a call covers (a band plus halo rows, or the whole frame).
+def conv3d(frames, weight, bias, out, *, Hin, Win, Cin, Cout, Tout, KT, KH, KW, stride_t=1, stride_hw=1,
+           pad=(0, 0, 0, 0), upsample=False, out_split=0, residual=None):
+    x = torch.stack([f.double() if f is not None else torch.zeros(Hin, Win, Cin, dtype=torch.float64) for f in frames])
+    x = x.permute(3, 0, 1, 2)[None]  # [1, C, F, H, W]
+    if upsample:
+        x = x.repeat_interleave(2, 3).repeat_interleave(2, 4)
+    top, left, bottom, right = pad
+    x = F.pad(x, (left, right, top, bottom))  # negative pads crop
+    w = weight.double().permute(0, 4, 1, 2, 3)  # [Cout, Cin, KT, KH, KW]
+    y = F.conv3d(x, w, None if bias is None else bias.double(), stride=(stride_t, stride_hw, stride_hw))[0, :, :Tout]
+    y = y.permute(1, 2, 3, 0)  # [Tout, Ho, Wo, Cout]
+    if out_split:  # time_conv of upsample3d: channel halves -> frames 2t, 2t + 1
+        y = y.reshape(Tout, y.shape[1], y.shape[2], 2, out_split).permute(0, 3, 1, 2, 4).reshape(2 * Tout, y.shape[1],
+                                                                                                   y.shape[2], out_split)
+    y = y.to(BF16)
+    if residual is not None:
+        y = (y.double() + residual.double()).to(BF16)
+    out.copy_(y)
+    return out
+
+
+def rms_norm_silu(x, gamma, silu=True, out=None):
+    xf = x.double()
+    y = xf / xf.norm(2, dim=-1, keepdim=True).clamp_min(1e-12) * (x.shape[-1] ** 0.5) * gamma.double()
+    if silu:
+        y = F.silu(y)
+    y = y.to(BF16)
+    if out is None:
+        return y
+    out.copy_(y)
+    return out
+
+
+def vae_attn(q, k, v, out=None, scale=None):
+    sc = q.shape[-1] ** -0.5 if scale is None else scale
+    p = torch.softmax(torch.einsum("tld,tmd->tlm", q.double(), k.double()) * sc, -1)
+    o = torch.einsum("tlm,tmd->tld", p, v.double()).to(BF16)
+    if out is None:
+        return o
+    out.copy_(o)
+    return out
+
+
+_FUNCS = dict(conv3d=conv3d, rms_norm_silu=rms_norm_silu, vae_attn=vae_attn, ln_mod=ln_mod, final_ln_mod=final_ln_mod, head_rmsnorm_rope=head_rmsnorm_rope, copy_rows=copy_rows,
               attn_fwd=attn_fwd, attn_kernel_name=attn_kernel_name, gemm_epi=gemm_epi, gemm_res=gemm_res, gelu_=gelu_)
 
 
