@@ -221,9 +221,13 @@ class MinimalV1LVGDiT:
         # the GELU and the residuals in the elementwise kernels (the round-2 path, kept for A/B)
         self.block_gemm = "own"
         # single-GPU self-attention with weight-based norm bounds past the zero-shift window (trained q/k norm weights):
-        # the k RMSNorm kernel measures max |k| (64 device slots) and the attention runs the gated pair, the
-        # zero-shift loop for every 256-query block whose data-tight bound allows it (cp25_attn_fwd_prescaled_kslots)
-        self.data_tight_k_bound = True
+        # True: the k RMSNorm kernel measures max |k| (64 device slots) and the attention runs the gated pair, the
+        # zero-shift loop for every 256-query block whose data-tight bound allows it (cp25_attn_fwd_prescaled_kslots).
+        # Off by default since round 4: with V staged by LDS-DMA the online-max form runs within 0.5 % of the zero-shift
+        # loop (profiles/r4/attn_dma, r4ab_*), and without the gate a row's arithmetic never depends on its 256-row
+        # block or on the other CFG entry's keys, so context-parallel shards stay bit-identical to CP = 1 with any
+        # checkpoint (tests/test_cp_gpu.py "nw_weight")
+        self.data_tight_k_bound = False
 
     def set_linear_precision(self, precision: str) -> None:
         """"bf16" (default, the reference's arithmetic) or "fp8": the 28 blocks' q/k/v, output, cross-q,

@@ -162,9 +162,14 @@ constexpr int kLds16 = 2 * kKBuf16 + 2 * kVBuf16;  // 73728
 // (boundary_probe_v1.log). Spread one piece per tile it measured slower still (every tile then waits on a piece,
 // boundary_probe_v2.log).
 constexpr bool kQCopyStagger = true;
-constexpr int kOStr = 272;                          // staged O row stride (256 B + 16: conflict-free b64 writes)
-constexpr int kQSlot = kQRows * kOStr;              // per wave 8704 B: next-block Q fragments (8 KiB) / staged O rows
-constexpr int kLdsP = kLds16 + kWaves * kQSlot;     // 143360
+// Staged O rows: 256 B per row, no padding, with the 8-B slots XOR-swizzled by the row's index within its 16-row half
+// (phys slot = slot ^ (row & 15)): the ds_write_b64 of a lane group (16 rows, one column) lands on 16 distinct 8-B bank
+// pairs, and a ds_read_b128 of logical 16-B chunk k reads physical chunk k ^ ((row & 15) >> 1) -- its two 8-B halves
+// swapped when the row is odd -- so the read groups are conflict-free too. (The round-3 272-B padded rows were 2-way
+// conflicted on both: 10.5 M SQ_LDS_BANK_CONFLICT cycles per launch, profiles/r3/pmc_s2.)
+constexpr int kOStr = 256;
+constexpr int kQSlot = kQRows * kOStr;              // per wave 8192 B: next-block Q fragments (8 KiB) / staged O rows
+constexpr int kLdsP = kLds16 + kWaves * kQSlot;     // 139264
 
 // kMode: 0 fixed shift, 1 fixed shift known to be 0 (pre-scaled q, bound product <= 96: no initial C), 2 online.
 // kGate (cp25_attn_fwd_prescaled_kslots: a data-tight key bound in device memory, the max |k| the producing RMSNorm
@@ -451,26 +456,31 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
 #pragma unroll
     for (int qh = 0; qh < 2; ++qh) {
       const float inv = 1.f / lsum[qh][0];
-      char* const wr = slot + (16 * qh + (lf & 15)) * kOStr + 8 * (lf >> 4);  // row 16 qh + c, d = 16 db + 4 g
+      // row 16 qh + c, d = 16 db + 4 g: logical 8-B slot 4 db + g, physical (4 db + g) ^ c
+      char* const wr = slot + (16 * qh + (lf & 15)) * kOStr;
 #pragma unroll
       for (int db = 0; db < 8; ++db) {
         u16x4 w;
 #pragma unroll
         for (int e = 0; e < 4; ++e) w[e] = f2bf(o[db][qh][e] * inv);
-        *reinterpret_cast<u16x4*>(wr + 32 * db) = w;
+        *reinterpret_cast<u16x4*>(wr + 8 * ((4 * db + (lf >> 4)) ^ (lf & 15))) = w;
       }
       lsum[qh] = zero4;
 #pragma unroll
       for (int db = 0; db < 8; ++db) o[db][qh] = zero4;
     }
     // store i: rows 4 i .. 4 i + 3 of the wave's 32, lane l row 4 i + l / 16, 16-B chunk l % 16 (one wave's LDS
-    // writes and reads execute in order)
-    const char* const rd = slot + (lf >> 4) * kOStr + 16 * (lf & 15);
+    // writes and reads execute in order). Row 4 i + h (h = l / 16) has (row & 15) >> 1 = 2 (i & 3) + (h >> 1): its
+    // physical chunk is (l % 16) ^ (h >> 1) ^ 2 (i & 3), halves swapped for odd h (a lane constant).
+    const char* const rd = slot + (lf >> 4) * kOStr;
+    const int kc = (lf & 15) ^ (lf >> 5);
+    const bool odd_row = (lf >> 4) & 1;
     unsigned short* const wo = const_cast<unsigned short*>(base) + 8 * (lf & 15);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int r = 4 * i + (lf >> 4);
-      const u32x4 v = *reinterpret_cast<const u32x4*>(rd + 4 * i * kOStr);
+      u32x4 v = *reinterpret_cast<const u32x4*>(rd + 4 * i * kOStr + 16 * (kc ^ (2 * (i & 3))));
+      if (odd_row) v = u32x4{v[2], v[3], v[0], v[1]};
       if (row0 + r < a.Lq) *reinterpret_cast<u32x4*>(wo + (int64_t)(row0 + r) * a.o_sl) = v;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read back before the next Q copy lands in the slot

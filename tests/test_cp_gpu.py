@@ -16,10 +16,10 @@ match the single-rank run (guidance 0, 2 Karras steps = 3 evals x CFG).
   fp8 attention too (q / k scales are fixed powers of two, V's per-head scale is taken over the gathered
   keys, which every rank holds whole).
 * trained-size q/k norm weights (uniform in [0.5, 3], bound product ~147): CP > 1 runs the online-max attention on the
-  weight bounds; CP = 1 by default runs the gated pair (data_tight_k_bound: zero shift for every 256-query block whose
-  measured bound allows it, chosen per block of the whole sequence, the max |k| taken over the whole CFG batch), so
-  the two round P at different shifts: bit-identity holds against CP = 1 with data_tight_k_bound = False ("nw_weight"),
-  and against the default CP = 1 the distance is rounding ("nw_gated", <= 1.5e-2 like the split plan's).
+  weight bounds, and so does CP = 1 by default (round 4): bit-identity ("nw_weight"). The opt-in gated pair at CP = 1
+  (data_tight_k_bound = True: zero shift for every 256-query block whose measured bound allows it, chosen per block of
+  the whole sequence, the max |k| taken over the whole CFG batch) rounds P at other shifts: against it the distance is
+  rounding ("nw_gated", <= 1.5e-2 like the split plan's).
 """
 import os
 import socket
@@ -119,8 +119,8 @@ def test_cp2_matches_cp1(device, monkeypatch, world, split_env, tol, precision):
     m.net.force_lanes = bool(split_env)
     if precision.startswith("nw_"):
         kern = m.net.attention_kernels(shape[1] * shape[2] * shape[3] // 4)
-        assert "gated" in kern["self"], kern  # CP = 1's default with these weights
-        m.net.data_tight_k_bound = precision == "nw_gated"  # nw_weight: the CP path's own (weight-bound) mode
+        assert "online" in kern["self"], kern  # CP = 1's default with these weights: the CP path's own mode
+        m.net.data_tight_k_bound = precision == "nw_gated"  # opt-in gated pair at CP = 1
     ref = _run(m, gt, cc, cu, shape, device)
     del m
     torch.cuda.empty_cache()
