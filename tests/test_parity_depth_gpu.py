@@ -182,3 +182,8 @@ def test_full_depth_2b_sampler(device, net2b, guidance):
     # reference's own distance from exact math, which is the scale of that amplification
     assert d["hip_truth"] <= 1.1 * d["ref_truth"], d
     assert d["hip_ref"] <= (1.6e-2 if guidance == 0 else 1.2 * d["ref_truth"]), d
+    # regression gates (round 4, VERDICT r3: the gates above cannot see a few-percent regression): the measured ratios
+    # with ~4 % margin -- g=0 hip-truth / ref-truth 1.001; g=7 1.013 and hip-ref / ref-truth 0.907
+    assert d["hip_truth"] <= 1.05 * d["ref_truth"], d
+    if guidance > 0:
+        assert d["hip_ref"] <= 0.95 * d["ref_truth"], d
