@@ -162,14 +162,17 @@ constexpr int kLds16 = 2 * kKBuf16 + 2 * kVBuf16;  // 73728
 // (boundary_probe_v1.log). Spread one piece per tile it measured slower still (every tile then waits on a piece,
 // boundary_probe_v2.log).
 constexpr bool kQCopyStagger = true;
-// Staged O rows: 256 B per row, no padding, with the 8-B slots XOR-swizzled by the row's index within its 16-row half
-// (phys slot = slot ^ (row & 15)): the ds_write_b64 of a lane group (16 rows, one column) lands on 16 distinct 8-B bank
-// pairs, and a ds_read_b128 of logical 16-B chunk k reads physical chunk k ^ ((row & 15) >> 1) -- its two 8-B halves
-// swapped when the row is odd -- so the read groups are conflict-free too. (The round-3 272-B padded rows were 2-way
-// conflicted on both: 10.5 M SQ_LDS_BANK_CONFLICT cycles per launch, profiles/r3/pmc_s2.)
-constexpr int kOStr = 256;
-constexpr int kQSlot = kQRows * kOStr;              // per wave 8192 B: next-block Q fragments (8 KiB) / staged O rows
-constexpr int kLdsP = kLds16 + kWaves * kQSlot;     // 139264
+// Staged O rows of 264 B (256 + 8): a ds_write_b64 lane group (16 rows, one 8-B column) lands on 16 distinct 8-B bank
+// pairs (row r at 33 r 8-B slots), and the rows are read back as two ds_read_b64 per 16-B chunk (8-B aligned rows: a
+// b128 read needs 16), lo halves then hi halves, each 16-lane group reading 8 chunks of two adjacent rows: the odd
+// 8-B shift between the rows puts one row's halves on the even slots and the other's on the odd ones, so every group
+// covers 16 distinct slots (and every 32-lane group 32): conflict-free with lane-constant addresses plus immediates.
+// Measured alternatives (profiles/r4/xattn/): round 3's 272-B rows, 2-way conflicted on the writes and the b128 reads
+// (10.5 M SQ_LDS_BANK_CONFLICT cycles per launch); an XOR-swizzled 256-B layout read by b128, conflict-free but its
+// per-read swizzle and half swap cost +1.3 %; 264-B rows read one row per 16 lanes, 7.0 M (chunks k and k + 8 collide).
+constexpr int kOStr = 264;
+constexpr int kQSlot = kQRows * kOStr;              // per wave 8448 B: next-block Q fragments (8 KiB) / staged O rows
+constexpr int kLdsP = kLds16 + kWaves * kQSlot;     // 141312
 
 // kMode: 0 fixed shift, 1 fixed shift known to be 0 (pre-scaled q, bound product <= 96: no initial C), 2 online.
 // kGate (cp25_attn_fwd_prescaled_kslots: a data-tight key bound in device memory, the max |k| the producing RMSNorm
@@ -456,32 +459,30 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
 #pragma unroll
     for (int qh = 0; qh < 2; ++qh) {
       const float inv = 1.f / lsum[qh][0];
-      // row 16 qh + c, d = 16 db + 4 g: logical 8-B slot 4 db + g, physical (4 db + g) ^ c
-      char* const wr = slot + (16 * qh + (lf & 15)) * kOStr;
+      char* const wr = slot + (16 * qh + (lf & 15)) * kOStr + 8 * (lf >> 4);  // row 16 qh + c, d = 16 db + 4 g
 #pragma unroll
       for (int db = 0; db < 8; ++db) {
         u16x4 w;
 #pragma unroll
         for (int e = 0; e < 4; ++e) w[e] = f2bf(o[db][qh][e] * inv);
-        *reinterpret_cast<u16x4*>(wr + 8 * ((4 * db + (lf >> 4)) ^ (lf & 15))) = w;
+        *reinterpret_cast<u16x4*>(wr + 32 * db) = w;
       }
       lsum[qh] = zero4;
 #pragma unroll
       for (int db = 0; db < 8; ++db) o[db][qh] = zero4;
     }
-    // store i: rows 4 i .. 4 i + 3 of the wave's 32, lane l row 4 i + l / 16, 16-B chunk l % 16 (one wave's LDS
-    // writes and reads execute in order). Row 4 i + h (h = l / 16) has (row & 15) >> 1 = 2 (i & 3) + (h >> 1): its
-    // physical chunk is (l % 16) ^ (h >> 1) ^ 2 (i & 3), halves swapped for odd h (a lane constant).
-    const char* const rd = slot + (lf >> 4) * kOStr;
-    const int kc = (lf & 15) ^ (lf >> 5);
-    const bool odd_row = (lf >> 4) & 1;
-    unsigned short* const wo = const_cast<unsigned short*>(base) + 8 * (lf & 15);
+    // store i: rows 4 i .. 4 i + 3 of the wave's 32; lane l: row 4 i + 2 (l / 32) + (l / 8) % 2, 16-B chunk
+    // 8 ((l / 16) % 2) + l % 8, read as two 8-B halves (one wave's LDS writes and reads execute in order)
+    const int rrow = 2 * (lf >> 5) + ((lf >> 3) & 1), rch = 8 * ((lf >> 4) & 1) + (lf & 7);
+    const char* const rd = slot + rrow * kOStr + 16 * rch;
+    unsigned short* const wo = const_cast<unsigned short*>(base) + 8 * rch;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int r = 4 * i + (lf >> 4);
-      u32x4 v = *reinterpret_cast<const u32x4*>(rd + 4 * i * kOStr + 16 * (kc ^ (2 * (i & 3))));
-      if (odd_row) v = u32x4{v[2], v[3], v[0], v[1]};
-      if (row0 + r < a.Lq) *reinterpret_cast<u32x4*>(wo + (int64_t)(row0 + r) * a.o_sl) = v;
+      const int r = 4 * i + rrow;
+      typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+      const u32x2 lo = *reinterpret_cast<const u32x2*>(rd + 4 * i * kOStr);
+      const u32x2 hi = *reinterpret_cast<const u32x2*>(rd + 4 * i * kOStr + 8);
+      if (row0 + r < a.Lq) *reinterpret_cast<u32x4*>(wo + (int64_t)(row0 + r) * a.o_sl) = u32x4{lo[0], lo[1], hi[0], hi[1]};
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read back before the next Q copy lands in the slot
   };
