@@ -1179,17 +1179,72 @@ int num_cus() {
 // MI355X measurements (tools/bench_cp_chunks.py: B 2, H 16, Lq 13640, Lk 109120 ran 21.9 ms unsplit vs 23.0 ms at
 // split 4; H 4: 6.24 vs 6.14 ms): shorter workgroups lose the lock-step K/V streaming through the XCD's L2 that
 // long ones keep. Picks the split with the least modelled time.
+// Cost of one split launch in tile-times (a workgroup's prologue / epilogue ~ 44 tiles; the fp32 partials' write,
+// read and merge at ~9 MB per tile-time): the plan's model.
+double split_cost(int64_t nwg, int64_t ntiles, int s, int64_t rows, int64_t cus) {
+  const int64_t tps = cdiv(ntiles, s);
+  double cost = (double)cdiv(nwg * s, cus) * (double)(tps + 44);
+  if (s > 1) cost += (2.0 * s + 0.5) * (double)rows * kD * 4 / 9.0e6;
+  return cost;
+}
+
+// Tail split of an unsplit self-attention launch. With nwg workgroups of equal length on cus CUs the last round runs
+// r = nwg % cus of them and leaves the other CUs idle for a whole workgroup time (the metric launch: 13 664 = 53 x 256
+// + 96, 1.2 % of the launch; a CP = 8 lane: 864 = 3 x 256 + 96, 11 %). The main launch then covers the first nwg - r
+// tiles (whole rounds) and the last r query blocks run as key-range splits (per (b, h) segment, s splits each chosen
+// to fill one round) with their partials merged, which shortens the tail round to ~1/s of a workgroup. TailSeg lists
+// the segments; returns their count (0: no tail split), the largest segment's workspace in *ws_need.
+struct TailSeg { int bh, qb_lo, nblk, s; };
+constexpr int kMaxTailSegs = 4;
+int plan_tail(int B, int H, int Lq, int Lk, TailSeg* seg, size_t* ws_need, double* saved) {
+  const int64_t nqb = cdiv(Lq, kQBlk), ntiles = cdiv(Lk, kKBlk);
+  const int64_t nwg = nqb * B * H, cus = num_cus();
+  const int64_t r = nwg % cus;
+  *ws_need = 0;
+  if (saved) *saved = 0.0;
+  if (r == 0 || nwg < cus || Lk <= 4096) return 0;
+  int n = 0;
+  double cost = 0.0;
+  size_t need = 0;
+  for (int64_t t = nwg - r; t < nwg;) {  // tiles in (b, h) > query block order
+    const int bh = (int)(t / nqb), qb = (int)(t % nqb);
+    const int nblk = (int)std::min<int64_t>(nqb - qb, nwg - t);
+    if (n == kMaxTailSegs) return 0;
+    int s = 1;
+    for (int c = 2; c <= 8 && c <= ntiles; ++c) {  // the most splits that still fit one round
+      const int64_t tps = cdiv(ntiles, c);
+      if (cdiv(ntiles, tps) == c && (int64_t)nblk * c <= cus) s = c;
+    }
+    if (s == 1) return 0;
+    const int64_t rows = std::min<int64_t>(Lq, (int64_t)(qb + nblk) * kQBlk) - (int64_t)qb * kQBlk;
+    seg[n++] = TailSeg{bh, qb, nblk, s};
+    cost += split_cost(nblk, ntiles, s, rows, cus) + 8.0;  // + launch overhead of the split and merge kernels
+    need = std::max<size_t>(need, (size_t)s * rows * (kD + 1) * sizeof(float));
+    t += nblk;
+  }
+  const double unsplit = (double)(ntiles + 44);  // the tail round as one round of whole workgroups
+  if (cost >= 0.9 * unsplit) return 0;
+  *ws_need = need;
+  if (saved) *saved = unsplit - cost;
+  return n;
+}
+
 int plan_split(int B, int H, int Lq, int Lk) {
   const int64_t nqb = cdiv(Lq, kQBlk), ntiles = cdiv(Lk, kKBlk);
   const int64_t nwg = nqb * B * H, cus = num_cus();
+  const int64_t rows = (int64_t)B * H * Lq;
   int best = 1;
   double best_cost = 1e300;
   for (int s = 1; s <= 8 && s <= ntiles; ++s) {
     const int64_t tps = cdiv(ntiles, s);
     if (cdiv(ntiles, tps) != s) continue;  // every split must own at least one tile
-    const double rounds = (double)cdiv(nwg * s, cus);
-    double cost = rounds * (double)(tps + 44);
-    if (s > 1) cost += (2.0 * s + 0.5) * (double)B * H * Lq * kD * 4 / 9.0e6;
+    double cost = split_cost(nwg, ntiles, s, rows, cus);
+    if (s == 1) {  // unsplit launches may run their last round as a tail split (plan_tail)
+      TailSeg seg[kMaxTailSegs];
+      size_t need;
+      double saved;
+      if (plan_tail(B, H, Lq, Lk, seg, &need, &saved) > 0) cost -= saved;
+    }
     if (cost < best_cost * 0.995) { best_cost = cost; best = s; }
   }
   return best;
@@ -1261,6 +1316,14 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
     if (!workspace || ((uintptr_t)workspace & 15) || ws_bytes < cp25_attn_workspace_bytes(B, H, Lq, n_split))
       return CP25_ERR_INVAL;
   }
+  // unsplit self-attention with a workspace (cp25_attn_tail_workspace_bytes): the last, partial round as a tail split
+  TailSeg tail[kMaxTailSegs];
+  int n_tail = 0;
+  if (n_split == 1 && fp8 == 0 && !kslots && workspace && !((uintptr_t)workspace & 15)) {
+    size_t need = 0;
+    n_tail = plan_tail(B, H, Lq, Lk, tail, &need, nullptr);
+    if (ws_bytes < need) n_tail = 0;
+  }
   AttnArgs a;
   a.q = (const unsigned short*)q; a.k = (const unsigned short*)k; a.v = (const unsigned short*)v;
   a.o = (unsigned short*)o;
@@ -1313,8 +1376,34 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
         if (mode == 2) M16(false, 2); else M16(false, 0);
       }
 #undef M16
+      if (n_tail) grid = nwg - nwg % num_cus();  // whole rounds; the rest below
     }
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kThreads), 0, stream, a);
+    CP25_LAUNCH_CHECK();
+    // tail segments: (b, h) = bh, query blocks [qb_lo, qb_lo + nblk), as a B = H = 1 problem of s key-range splits on
+    // the same kernel, its fp32 partials in the workspace, merged into o (the same arithmetic as any split launch)
+    for (int i = grid < nwg ? 0 : n_tail; i < n_tail; ++i) {
+      const TailSeg& g = tail[i];
+      const int b = g.bh / H, h = g.bh % H;
+      const int64_t row0 = (int64_t)g.qb_lo * kQBlk;
+      AttnArgs t = a;
+      t.q = a.q + b * a.q_sb + h * a.q_sh + row0 * a.q_sl;
+      t.k = a.k + b * a.k_sb + h * a.k_sh;
+      t.v = a.v + b * a.v_sb + h * a.v_sh;
+      t.o = a.o + b * a.o_sb + h * a.o_sh + row0 * a.o_sl;
+      t.B = 1; t.H = 1;
+      t.Lq = (int)(std::min<int64_t>(Lq, row0 + (int64_t)g.nblk * kQBlk) - row0);
+      t.nqb = g.nblk;
+      t.nsplit = g.s;
+      t.tps = (int)cdiv(ntiles, g.s);
+      t.o_part = (float*)workspace;
+      t.lse_part = (float*)workspace + (size_t)g.s * t.Lq * kD;
+      hipLaunchKernelGGL(kern, dim3((unsigned)(g.nblk * g.s)), dim3(kThreads), 0, stream, t);
+      CP25_LAUNCH_CHECK();
+      hipLaunchKernelGGL(attn_merge_splits, dim3((unsigned)cdiv((int64_t)t.Lq * 32, 256)), dim3(256), 0, stream,
+                         t.o_part, t.lse_part, t.o, g.s, 1, 1, t.Lq, a.o_sb, a.o_sl, a.o_sh);
+      CP25_LAUNCH_CHECK();
+    }
   }
   CP25_LAUNCH_CHECK();
   if (n_split > 1) {
@@ -1348,6 +1437,13 @@ extern "C" int cp25_attn_fwd_prescaled_fp8(const void* q8, const void* k8, const
 extern "C" size_t cp25_attn_workspace_bytes(int B, int H, int Lq, int n_split) {
   if (n_split <= 1 || B <= 0 || H <= 0 || Lq <= 0) return 0;
   return (size_t)n_split * B * H * Lq * (kD + 1) * sizeof(float);
+}
+
+extern "C" size_t cp25_attn_tail_workspace_bytes(int B, int H, int Lq, int Lk) {
+  if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0) return 0;
+  TailSeg seg[kMaxTailSegs];
+  size_t need = 0;
+  return plan_tail(B, H, Lq, Lk, seg, &need, nullptr) > 0 ? need : 0;
 }
 
 extern "C" int cp25_attn_plan(int B, int H, int Lq, int Lk, int D) {

@@ -137,6 +137,13 @@ const char* cp25_attn_kernel(int Lk, float softmax_scale, float q_norm_bound, fl
 /* Bytes of workspace cp25_attn_fwd_split / _bounded need (0 for n_split <= 1). */
 size_t cp25_attn_workspace_bytes(int B, int H, int Lq, int n_split);
 
+/* Bytes of workspace with which an unsplit (n_split = 1) bf16 self-attention launch of _split / _bounded / _prescaled
+ * (Lk > 4096, no key-norm slots) runs its last, partial round of workgroups as a tail split: the first
+ * (nwg - nwg % CUs) query blocks as one launch of whole rounds, the remaining ones as key-range splits merged into o
+ * (the split launches' arithmetic). 0 when the shape has no such tail or it would not pay. Passing less (or no
+ * workspace) runs the launch whole, as one grid. */
+size_t cp25_attn_tail_workspace_bytes(int B, int H, int Lq, int Lk);
+
 /* The key-range split the library picks for this shape on the current device (>= 1; a round model of
  * one workgroup per CU), or a negative error code. */
 int cp25_attn_plan(int B, int H, int Lq, int Lk, int D);

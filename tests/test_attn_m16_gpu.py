@@ -219,3 +219,36 @@ def test_m16_zero_shift_top_of_window_long_keys(device):
     assert torch.isfinite(o.float()).all()
     mean_v = v.float().mean(1)[0, 0]
     assert rel_l2(o[0, :, 0], mean_v.expand(Lq, 128)) <= 2 ** -8
+
+
+@pytest.mark.parametrize("prescaled", [False, True])
+def test_m16_tail_split(device, prescaled):
+    """The last, partial round of an unsplit launch as a tail split (cp25_attn_tail_workspace_bytes): a CP = 8 lane's
+    shape (B 1, H 16, 13 640 queries: 864 = 3 x 256 + 96 workgroups) with 32 768 keys. The first 768 query blocks run in
+    the main launch, bit-identical to the whole unsplit launch; the last 96 (head 14 from block 12, and head 15) as
+    key-range splits merged into o, within rounding of it and as close to fp32 (rows of both tail segments)."""
+    B, H, Lq, Lk = 1, 16, 13640, 32768
+    lib = N.load_library()
+    assert lib.cp25_attn_tail_workspace_bytes(B, H, Lq, Lk) > 0 and N.attn_plan(B, H, Lq, Lk) == 1
+    q, k, v = _inputs(device, B, H, Lq, Lk, 77)
+    if prescaled:
+        q = (q.float() * 128 ** -0.5 * LOG2E).to(torch.bfloat16)
+        kw, scale = dict(prescaled=True), 1.0 / LOG2E
+    else:
+        kw, scale = {}, 128 ** -0.5
+    whole = N.attn_fwd(q, k, v, n_split=1, **kw)  # a given split: one grid, no tail
+    tail = N.attn_fwd(q, k, v, **kw)  # the library's plan: main rounds + tail split
+    torch.cuda.synchronize()
+    t0 = 12 * 256
+    assert torch.equal(tail[:, :, :14], whole[:, :, :14])
+    assert torch.equal(tail[:, :t0, 14], whole[:, :t0, 14])
+    e_tail = rel_l2(tail[:, t0:, 14:], whole[:, t0:, 14:])
+    rows = torch.cat([torch.arange(t0, t0 + 40), torch.arange(Lq - 40, Lq)]).to(device)
+    errs = {}
+    for h in (14, 15):
+        ref = ref_attention(q[:, rows, h:h + 1], k[:, :, h:h + 1], v[:, :, h:h + 1], scale)
+        errs[h] = (rel_l2(tail[:, rows, h:h + 1], ref), rel_l2(whole[:, rows, h:h + 1], ref))
+    print(f"tail split rows vs the whole launch {e_tail:.2e}; tail / whole vs fp32 {errs}")
+    assert 0 < e_tail <= 1.5 * TOL  # two independent bf16 roundings of P (each split has its own shift)
+    for h, (et, ew) in errs.items():
+        assert et <= TOL and ew <= TOL, errs
