@@ -2,7 +2,10 @@
 results are WRONG for every patch except 'none'). The product source is not touched: the patched copy is compiled from
 /tmp and linked with the in-tree objects of the other translation units.
 usage: python tools/lab/gemm_variant.py <name> <patch>[,<patch>...]  ->  tools/lab/libcp25_<name>.so
-patches: nostage (accumulators not written to the LDS C image), nostore (no global C stores), none"""
+patches: nostage (accumulators not written to the LDS C image), nostore (no global C stores), none;
+correct-result variants: sc1 (full-tile C stores write-through, dropping the lines from the XCD L2, via a buffer
+store with the sc1 policy bit), stagger<N> (workgroup w sleeps ((w >> 3) & 15) x s_sleep N before its first tile, so
+the workgroups' tile seams -- and their C-store bursts -- no longer coincide chip-wide)"""
 import os
 import subprocess
 import sys
@@ -12,12 +15,22 @@ CSRC = os.path.join(ROOT, "cosmos-predict2.5_amd", "csrc")
 OBJ = os.path.join(ROOT, "cosmos-predict2.5_amd", "cosmos_predict2", "_lib", "obj")
 
 PATCHES = {
-    "nostage": [("              stj[j][(mq * 128 + 16 * i + r) * 256 + nq * 128] = f2bf(y);\n",
-                 "              if (y == 12345.f) stj[j][(mq * 128 + 16 * i + r) * 256 + nq * 128] = f2bf(y);\n")],
+    "nostage": [("                stj[j][(mq * 128 + 16 * i + r) * 256 + nq * 128] = f2bf(rbf(a));\n",
+                 "                if (a == 12345.f) stj[j][(mq * 128 + 16 * i + r) * 256 + nq * 128] = f2bf(rbf(a));\n")],
     "nostore": [("      for (int it = 0; it < 16; ++it) *reinterpret_cast<u32x4*>(crow + (int64_t)it * 16 * ldc) = cv[it];\n",
                  "      for (int it = 0; it < 16; ++it) if (cv[it][0] == 0x12345678u) *reinterpret_cast<u32x4*>(crow + (int64_t)it * 16 * ldc) = cv[it];\n")],
+    "sc1": [("    unsigned short* crow = C + (int64_t)(m0 + r0) * ldc + n0 + ch * 8;\n",
+             "    unsigned short* crow = C + (int64_t)(m0 + r0) * ldc + n0 + ch * 8;\n"
+             "    const auto c_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(C + (int64_t)m0 * ldc + n0), (short)0, 0x7fffffff, 0x00020000);\n"
+             "    const int c_off = (r0 * (int)ldc + ch * 8) * 2;\n"),
+            ("      for (int it = 0; it < 16; ++it) *reinterpret_cast<u32x4*>(crow + (int64_t)it * 16 * ldc) = cv[it];\n",
+             "      for (int it = 0; it < 16; ++it) __builtin_amdgcn_raw_buffer_store_b128(cv[it], c_rsrc, c_off + it * 16 * (int)ldc * 2, 0, 16);\n")],
     "none": [],
 }
+for _n in (4, 8, 16, 32):
+    PATCHES[f"stagger{_n}"] = [("  if (tile >= n_tiles) return;\n",
+                                "  if (tile >= n_tiles) return;\n"
+                                f"  for (int d = (blockIdx.x >> 3) & 15; d > 0; --d) __builtin_amdgcn_s_sleep({_n});\n")]
 
 
 def main():
