@@ -12,16 +12,17 @@
 //     query on the lane, Q^T fragments resident in 96 VGPRs), then O^T = V^T P^T with the S accumulator
 //     converted to bf16 in place as the B operand and V^T read by ds_read_b64_tr_b16; O^T is 12 d-blocks of
 //     32 x 32 (192 accumulators);
-//   * two passes over the keys: the exact row max (Q K^T only), then P = exp2(S c - m) with that fixed shift,
-//     so O^T is never rescaled and stays in the accumulator file (192 registers next to the 96 of Q^T);
-//     P rounded to bf16 for P V as flash kernels do;
+//   * one pass over the keys with the softmax shift fixed at the first key tile's row max, so O^T is never
+//     rescaled and stays in the accumulator file (192 registers next to the 96 of Q^T); a workgroup whose rows see
+//     a later tile max more than 2^24 above that shift redoes its block with the exact row max of all keys (a
+//     Q K^T-only pass first, round 3's form); P rounded to bf16 for P V as flash kernels do;
 //   * K/V stream through LDS in 32-key tiles (24 KB each), double-buffered, register-staged by all 256
 //     threads one tile ahead; padded rows (K 784 B, V 832 B) keep the K row reads and the transposed V reads
 //     bank-conflict-free (the same padding rule as attn_fwd.hip's 272 / 320 B rows at d = 128).
 //   * when the query blocks alone do not cover the CUs (one frame: 110 blocks), the keys are split over up to
 //     8 workgroups per block (flash-decoding); each writes (O, m, l) partials and vae_attn_combine merges them.
-// Numerics: fp32 scores / max / sum, bf16 P, fp32 O normalised once and rounded to bf16 (the same values a
-// one-pass online softmax reaches once its running max is final).
+// Numerics: fp32 scores / max / sum, bf16 P (terms <= 2^24 after the shift), fp32 O normalised once and rounded to
+// bf16.
 #include "cp25_common.h"
 
 namespace {
@@ -37,6 +38,7 @@ constexpr int kVVBuf = kVKeys * kVVStride;  // 26624
 constexpr int kVStage = kVKBuf + kVVBuf;
 constexpr int kVChunks = kVKeys * kVD / 8;  // 16-B chunks per K (or V) tile: 1536
 constexpr int kVPerThread = kVChunks / 256;  // 6
+constexpr float kVLazy = 24.f;              // one-pass form: largest exponent a term may reach past the first tile's max
 
 struct VaeAttnArgs {
   const unsigned short* q;
@@ -49,8 +51,13 @@ struct VaeAttnArgs {
   float scale_log2;                    // softmax scale * log2(e)
   int splits;                          // key splits (grid.z): > 1 writes partials to ws for vae_attn_combine
   float* ws;                           // [splits][T][Lq][D + 2] fp32: O (unnormalised), m, l
+  int* flags;                          // [splits][T][query blocks]: the one-pass form overflowed (kFix redoes)
 };
 
+// kFix = false: the one-pass form; a workgroup whose first-tile shift a later tile overflows writes flags[wg] = 1 and
+// no output. kFix = true (launched next on the same stream): such workgroups (any other exits at once) redo the block
+// with the exact row max of all keys (a Q K^T-only pass, then the P V pass with that shift).
+template <bool kFix>
 __global__ void __launch_bounds__(256, 1) vae_attn_kernel(VaeAttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kVStage];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -66,6 +73,10 @@ __global__ void __launch_bounds__(256, 1) vae_attn_kernel(VaeAttnArgs a) {
   const int nt_all = (a.Lk + kVKeys - 1) / kVKeys;
   const int t_begin = (int)((int64_t)nt_all * blockIdx.z / a.splits);
   const int t_end = (int)((int64_t)nt_all * (blockIdx.z + 1) / a.splits);
+  const int64_t wg = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  if constexpr (kFix) {
+    if (a.flags[wg] == 0) return;  // the one-pass launch finished this block
+  }
 
   // Q^T fragments (B operand of S^T = K Q^T): lane (query l31, d 16 s + 8 hl .. + 8), 96 VGPRs
   bf16x8 qf[kVKS];
@@ -130,71 +141,100 @@ __global__ void __launch_bounds__(256, 1) vae_attn_kernel(VaeAttnArgs a) {
     return S;
   };
 
-  // ---- pass 1: the exact row max over all keys (Q K^T only). With it fixed, pass 2 never rescales O, so O stays
-  // in the accumulator file and is touched only by MFMAs (a running-max rescale would need all 192 values in
-  // VGPRs next to the Q^T fragments). Costs 1.5x the MFMAs of a single pass; the round-1 path's 793 MB score
-  // matrix per frame is gone.
-  float mx = -INFINITY;
-  load_tile(t_begin, false);
-  write_tile(0, false);
-  __syncthreads();
-  for (int t = t_begin; t < t_end; ++t) {
-    const int buf = (t - t_begin) & 1;
-    if (t + 1 < t_end) load_tile(t + 1, false);
-    const f32x16 S = scores(smem + buf * kVStage, t);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, S[r]);
-    if (t + 1 < t_end) write_tile(buf ^ 1, false);  // tile t - 1's buffer: every wave passed the last barrier
-    __syncthreads();
-  }
-  mx = fmaxf(mx, __shfl_xor(mx, 32));
-  const float m_row = mx * a.scale_log2;
-
-  // ---- pass 2: P = exp2(S c - m), l += sum P, O^T += V^T P^T
+  // ---- P V pass: P = exp2(S c - m), l += sum P, O^T += V^T P^T with a shift m fixed for the whole pass, so O is
+  // never rescaled and stays in the accumulator file (a rescale of the 192 accumulators inside the loop spilled).
+  // kOnline: m is the first tile's row max, and the pass reports (wave-uniform) whether a later tile's row max
+  // exceeded it by more than kVLazy (P would pass 2^24): then the kFix launch redoes the block with the exact row max
+  // of all keys (a Q K^T-only pass first, 1.5x the MFMAs, round 3's only form). Keys of one frame rarely do. (The
+  // redo inside the same kernel spilled: two inlined copies of this pass.)
   f32x16 o[kVDB];
+  float l_run = 0.f, m_row = -INFINITY;
+  auto pv_pass = [&](auto online_c) __attribute__((always_inline)) {
+    constexpr bool kOnline = decltype(online_c)::value;
+    bool ovf = false;
 #pragma unroll
-  for (int d = 0; d < kVDB; ++d)
+    for (int d = 0; d < kVDB; ++d)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
-  float l_run = 0.f;
-  load_tile(t_begin, true);
-  write_tile(0, true);
-  __syncthreads();
-  for (int t = t_begin; t < t_end; ++t) {
-    const int buf = (t - t_begin) & 1;
-    if (t + 1 < t_end) load_tile(t + 1, true);
-    const f32x16 S = scores(smem + buf * kVStage, t);
-    bf16x8 pb[2];
-#pragma unroll
-    for (int sp = 0; sp < 2; ++sp)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float p = __builtin_amdgcn_exp2f(fmaf(S[8 * sp + j], a.scale_log2, -m_row));
-        l_run += p;
-        pb[sp][j] = static_cast<__bf16>(p);
-      }
-    const char* vb = smem + buf * kVStage + v_rd;
-    auto v_frag = [&](int ks, int d) __attribute__((always_inline)) {
-      typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-      typedef __attribute__((address_space(3))) const char* lds_cptr;
-      const int off = 16 * ks * kVVStride + 64 * d;
-      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds_cptr)(vb + off));
-      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds_cptr)(vb + off + 8 * kVVStride));
-      typedef short s16x8 __attribute__((ext_vector_type(8)));
-      const s16x8 r8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      return __builtin_bit_cast(bf16x8, r8);
-    };
-    bf16x8 vr[3];
-    vr[0] = v_frag(0, 0);
-    vr[1] = v_frag(0, 1);
-#pragma unroll
-    for (int i = 0; i < 2 * kVDB; ++i) {
-      if (i + 2 < 2 * kVDB) vr[(i + 2) % 3] = v_frag((i + 2) / kVDB, (i + 2) % kVDB);
-      o[i % kVDB] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vr[i % 3], pb[i / kVDB], o[i % kVDB], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (t + 1 < t_end) write_tile(buf ^ 1, true);
+      for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+    l_run = 0.f;
+    load_tile(t_begin, true);
+    write_tile(0, true);
     __syncthreads();
+    for (int t = t_begin; t < t_end; ++t) {
+      const int buf = (t - t_begin) & 1;
+      if (t + 1 < t_end) load_tile(t + 1, true);
+      const f32x16 S = scores(smem + buf * kVStage, t);
+      if constexpr (kOnline) {
+        float tmax = S[0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) tmax = fmaxf(tmax, S[r]);
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32)) * a.scale_log2;  // the row's (lanes l31, l31 + 32) tile max
+        if (t == t_begin)
+          m_row = tmax;
+        else
+          ovf = ovf || __any(tmax > m_row + kVLazy);
+      }
+      bf16x8 pb[2];
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(S[8 * sp + j], a.scale_log2, -m_row));
+          l_run += p;
+          pb[sp][j] = static_cast<__bf16>(p);
+        }
+      const char* vb = smem + buf * kVStage + v_rd;
+      auto v_frag = [&](int ks, int d) __attribute__((always_inline)) {
+        typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+        typedef __attribute__((address_space(3))) const char* lds_cptr;
+        const int off = 16 * ks * kVVStride + 64 * d;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds_cptr)(vb + off));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds_cptr)(vb + off + 8 * kVVStride));
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        const s16x8 r8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(bf16x8, r8);
+      };
+      bf16x8 vr[3];
+      vr[0] = v_frag(0, 0);
+      vr[1] = v_frag(0, 1);
+#pragma unroll
+      for (int i = 0; i < 2 * kVDB; ++i) {
+        if (i + 2 < 2 * kVDB) vr[(i + 2) % 3] = v_frag((i + 2) / kVDB, (i + 2) % kVDB);
+        o[i % kVDB] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vr[i % 3], pb[i / kVDB], o[i % kVDB], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (t + 1 < t_end) write_tile(buf ^ 1, true);
+      __syncthreads();
+    }
+    return ovf;
+  };
+
+  if constexpr (!kFix) {
+    __shared__ int redo;     // any wave of the workgroup overflowed the first-tile shift
+    if (tid == 0) redo = 0;  // ordered before the waves' writes by the pass's first barrier
+    const bool ovf = pv_pass(std::true_type{});
+    if (ovf && lane == 0) redo = 1;
+    __syncthreads();
+    if (tid == 0) a.flags[wg] = redo;
+    if (redo) return;  // the kFix launch writes this block
+  } else {
+    // the exact row max over all keys (Q K^T only), then the P V pass with it
+    float mx = -INFINITY;
+    load_tile(t_begin, false);
+    write_tile(0, false);
+    __syncthreads();
+    for (int t = t_begin; t < t_end; ++t) {
+      const int buf = (t - t_begin) & 1;
+      if (t + 1 < t_end) load_tile(t + 1, false);
+      const f32x16 S = scores(smem + buf * kVStage, t);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, S[r]);
+      if (t + 1 < t_end) write_tile(buf ^ 1, false);  // tile t - 1's buffer: every wave passed the last barrier
+      __syncthreads();
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    m_row = mx * a.scale_log2;
+    pv_pass(std::false_type{});
   }
 
   // ---- epilogue: O^T lane (query l31), register r of d-block d holds d = 32 d + 8 (r / 4) + 4 hl + r % 4
@@ -267,10 +307,15 @@ int vae_attn_splits(int T, int Lq, int Lk) {
 
 }  // namespace
 
+// workspace: the per-workgroup overflow flags (rounded to 256 B), then the key-split partials when splits > 1
+static int64_t vae_attn_flag_bytes(int T, int Lq, int Lk) {
+  return ((int64_t)vae_attn_splits(T, Lq, Lk) * T * cdiv(Lq, 128) * 4 + 255) / 256 * 256;
+}
+
 extern "C" int64_t cp25_vae_attn_workspace_bytes(int T, int Lq, int Lk, int D) {
   if (T <= 0 || Lq <= 0 || Lk <= 0 || D != kVD) return 0;
   const int s = vae_attn_splits(T, Lq, Lk);
-  return s > 1 ? (int64_t)s * T * Lq * (kVD + 2) * 4 : 0;
+  return vae_attn_flag_bytes(T, Lq, Lk) + (s > 1 ? (int64_t)s * T * Lq * (kVD + 2) * 4 : 0);
 }
 
 extern "C" int cp25_vae_attn(const void* q, int64_t ldq, int64_t fq, const void* k, int64_t ldk, int64_t fk,
@@ -283,8 +328,7 @@ extern "C" int cp25_vae_attn(const void* q, int64_t ldq, int64_t fq, const void*
   if ((((uintptr_t)q) | ((uintptr_t)k) | ((uintptr_t)v) | ((uintptr_t)o)) & 15) return CP25_ERR_INVAL;
   if (T > 65535) return CP25_ERR_INVAL;
   const int splits = vae_attn_splits(T, Lq, Lk);
-  if (splits > 1 && (!workspace || workspace_bytes < cp25_vae_attn_workspace_bytes(T, Lq, Lk, D) ||
-                     ((uintptr_t)workspace & 15)))
+  if (!workspace || workspace_bytes < cp25_vae_attn_workspace_bytes(T, Lq, Lk, D) || ((uintptr_t)workspace & 15))
     return CP25_ERR_INVAL;
   VaeAttnArgs a;
   a.q = (const unsigned short*)q;
@@ -296,13 +340,16 @@ extern "C" int cp25_vae_attn(const void* q, int64_t ldq, int64_t fq, const void*
   a.Lq = Lq; a.Lk = Lk;
   a.scale_log2 = scale * 1.4426950408889634f;
   a.splits = splits;
-  a.ws = (float*)workspace;
-  hipLaunchKernelGGL(vae_attn_kernel, dim3((unsigned)cdiv(Lq, 128), (unsigned)T, (unsigned)splits), dim3(256), 0,
-                     stream, a);
+  a.flags = (int*)workspace;
+  a.ws = (float*)((char*)workspace + vae_attn_flag_bytes(T, Lq, Lk));
+  const dim3 grid((unsigned)cdiv(Lq, 128), (unsigned)T, (unsigned)splits);
+  hipLaunchKernelGGL(vae_attn_kernel<false>, grid, dim3(256), 0, stream, a);
+  CP25_LAUNCH_CHECK();
+  hipLaunchKernelGGL(vae_attn_kernel<true>, grid, dim3(256), 0, stream, a);
   CP25_LAUNCH_CHECK();
   if (splits > 1) {
     hipLaunchKernelGGL(vae_attn_combine, dim3((unsigned)cdiv((int64_t)T * Lq, 4)), dim3(256), 0, stream,
-                       (const float*)workspace, splits, T, Lq, (unsigned short*)o, ldo, fo);
+                       (const float*)a.ws, splits, T, Lq, (unsigned short*)o, ldo, fo);
     CP25_LAUNCH_CHECK();
   }
   return CP25_OK;

@@ -331,12 +331,13 @@ int cp25_rms_norm_silu(const void* x, const void* gamma, void* y, int64_t n_pix,
 /* o = softmax(q k^T * scale) v per frame, one head of D = 384 (the Wan VAE AttentionBlock), bf16 in / out, fp32
  * scores and sums, bf16 P. q [T][Lq][D], k / v [T][Lk][D], o [T][Lq][D] given as base pointers with row strides
  * (ld*) and frame strides (f*) in elements (multiples of 8, 16-B aligned bases), so q / k / v can be column
- * slices of the to_qkv output [T][L][3D]. Flash kernel (no score matrix in HBM): two passes over the keys
- * (exact row max, then exp / sum / P V). Replaces F.scaled_dot_product_attention in AttentionBlock.forward
- * (tokenizers/wan2pt1.py:225-261, q, k, v = [b*t, 1, h*w, c]). Returns CP25_ERR_DTYPE for D != 384.
- * When the query blocks do not cover the GPU the keys are split over several workgroups, whose partials go to
- * `workspace` (cp25_vae_attn_workspace_bytes(T, Lq, Lk, D) bytes, 16-B aligned; 0 = none needed) and are merged
- * by a second kernel on the same stream. */
+ * slices of the to_qkv output [T][L][3D]. Flash kernel (no score matrix in HBM): one pass over the keys with the
+ * softmax shift fixed at the first key tile's row max; a query block whose later scores exceed it by more than 2^24
+ * is redone by a second launch with the exact row max of all keys. Replaces F.scaled_dot_product_attention in
+ * AttentionBlock.forward (tokenizers/wan2pt1.py:225-261, q, k, v = [b*t, 1, h*w, c]). Returns CP25_ERR_DTYPE for
+ * D != 384. `workspace` (cp25_vae_attn_workspace_bytes(T, Lq, Lk, D) bytes, 16-B aligned, required) holds the
+ * per-block redo flags and, when the query blocks do not cover the GPU and the keys are split over several
+ * workgroups, their partials, merged by a further kernel on the same stream. */
 int64_t cp25_vae_attn_workspace_bytes(int T, int Lq, int Lk, int D);
 int cp25_vae_attn(const void* q, int64_t ldq, int64_t fq, const void* k, int64_t ldk, int64_t fk, const void* v,
                   int64_t ldv, int64_t fv, void* o, int64_t ldo, int64_t fo, int T, int Lq, int Lk, int D, float scale,

@@ -5,7 +5,8 @@ q / k / v [b*t, 1, h*w, 384] (flash / efficient backends: fp32 scores and sums, 
 vs fp32 softmax(q k^T / sqrt(384)) v of the same bf16 inputs (bf16 P + one output rounding; measured printed).
 Covers strided column slices of a [T, L, 3C] to_qkv buffer (the product's call), T > 1, ragged Lq / Lk (not a
 multiple of the 128-query block or the 32-key tile), Lk != Lq (the banded decode's gathered keys), and a
-row whose scores span a wide range (the exact-max pass keeps exp2 in range).
+row whose scores span a wide range: a key far above the first key tile's maximum overflows the one-pass shift,
+so its query blocks take the exact-max redo launch.
 """
 import pytest
 import torch

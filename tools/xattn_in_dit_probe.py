@@ -1,0 +1,94 @@
+"""The text cross-attention inside the DiT vs the same launch replayed alone. Builds the bench's pipeline (2B,
+720p x 121f, random weights), runs one evaluation with cp25 attention calls against the 512 text keys timed by HIP
+events, keeps the last call's operands, then replays that call alone (same tensors), on cloned operands, and
+back to back. One JSON line.
+usage: python tools/xattn_in_dit_probe.py"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "cosmos-predict2.5_amd"))
+
+import torch  # noqa: E402
+
+from cosmos_predict2 import _native as N  # noqa: E402
+from cosmos_predict2.pipeline import DEFAULT_NEGATIVE_PROMPT, Video2WorldInference  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    N.load_library()
+    h, w, frames = 704, 1280, 121
+    state_t = 1 + (frames - 1) // 4
+    pipe = Video2WorldInference("2B/post-trained", device=dev, state_t=state_t)
+    model = pipe.model
+    nf = model.tokenizer.get_pixel_num_frames(state_t)
+    rng = np.random.RandomState(3)
+    vid = torch.zeros(1, 3, nf, h, w, dtype=torch.uint8)
+    vid[0, :, 0] = torch.from_numpy(rng.randint(0, 256, size=(3, h, w), dtype=np.uint8))
+    batch = pipe._get_data_batch_input(vid, "A robot arm pours coffee into a mug on a kitchen counter.", 1,
+                                       DEFAULT_NEGATIVE_PROMPT)
+    state_shape = (model.config.state_ch, state_t, h // 8, w // 8)
+    real = N.attn_fwd
+    rec = {"calls": []}
+    last = {}
+
+    def spy(q, k, v, out=None, **kw):
+        if k.shape[1] != 512:
+            return real(q, k, v, out=out, **kw)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        r = real(q, k, v, out=out, **kw)
+        e1.record()
+        rec["calls"].append((e0, e1))
+        last.update(q=q, k=k, v=v, out=out, kw=kw)
+        return r
+
+    with torch.no_grad():
+        gt = model.encode_conditioning(batch["video"], 1, state_t)
+        run = model.begin_sampling(gt, batch["t5_text_embeddings"], batch["neg_t5_text_embeddings"],
+                                   state_shape=state_shape, num_conditional_frames=1, guidance=7, seed=0, num_steps=35)
+        run.step()
+        run.step()
+        torch.cuda.synchronize()
+        N.attn_fwd = spy
+        run.step()
+        torch.cuda.synchronize()
+        N.attn_fwd = real
+        ms = [e0.elapsed_time(e1) for e0, e1 in rec.pop("calls")]
+        rec["in_dit_ms"] = [round(x, 4) for x in ms]
+        rec["in_dit_mean_blocks_1_27"] = sum(ms[1:]) / len(ms[1:])
+        q, k, v, out, kw = last["q"], last["k"], last["v"], last["out"], last["kw"]
+        rec["layout"] = {"q": [list(q.shape), list(q.stride())], "k": [list(k.shape), list(k.stride())],
+                         "out": [list(out.shape), list(out.stride())], "kw": {a: str(b) for a, b in kw.items()}}
+
+        def timed(fn, n=10):
+            ts = []
+            for _ in range(n):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                fn()
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            return {"mean_ms": sum(ts) / n, "min_ms": min(ts)}
+
+        rec["replay_same_tensors"] = timed(lambda: real(q, k, v, out=out, **kw))
+        qc = q.clone(memory_format=torch.contiguous_format)
+        kc, vc = k.contiguous(), v.contiguous()
+        oc = torch.empty_like(qc)
+        rec["replay_contiguous_clones"] = timed(lambda: real(qc, kc, vc, out=oc, **kw))
+        # the DiT's exact strides on fresh storage: q / o as [B, n, H, hd] views of [n, B, H, hd] buffers
+        qs = torch.empty(q.shape[1], q.shape[0], q.shape[2], q.shape[3], device=dev, dtype=q.dtype)
+        qs.copy_(q.transpose(0, 1))
+        os_ = torch.empty_like(qs)
+        rec["replay_dit_strides_fresh"] = timed(lambda: real(qs.transpose(0, 1), kc, vc, out=os_.transpose(0, 1), **kw))
+    print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()
