@@ -65,6 +65,8 @@ SIGNATURES = {
                                     _P, ctypes.c_size_t, _P],
     "cp25_v_fp8t_bytes": [_I, _I, _I],
     "cp25_cast_v_fp8t": [_P, c_int64_p, _I, _I, _I, _I, _P, _P, _P],
+    "cp25_attn_fwd_prescaled_qnorm": [_P, _P, _P, _P, _I, _I, _I, _I, _I, c_int64_p, c_int64_p, c_int64_p, c_int64_p, _F,
+                                      _F, _P, _I, _P, _P, _P, _F, _F, _I, _P, ctypes.c_size_t, _P],
     "cp25_attn_workspace_bytes": [_I, _I, _I, _I],
     "cp25_attn_tail_workspace_bytes": [_I, _I, _I, _I],
     "cp25_attn_kernel": [_I, _F, _F, _F, _I, _I],
@@ -184,7 +186,7 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
              norm_bounds: Optional[Tuple[float, float]] = None, prescaled: bool = False,
              fp8_qk: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
              fp8_v: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-             k_norm_slots: Optional[torch.Tensor] = None) -> torch.Tensor:
+             k_norm_slots: Optional[torch.Tensor] = None, q_norm: Optional[dict] = None) -> torch.Tensor:
     """softmax(q k^T * scale) v for q [B, Lq, H, 128], k/v [B, Lk, H, 128] (bf16, any strides with
     a contiguous head dim). Returns [B, Lq, H, 128] bf16. n_split: key-range split (None = the
     library's plan for this shape; the fp32 partials live in a caching-allocator workspace).
@@ -198,7 +200,11 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
     e4m3 V too (cp25_attn_fwd_prescaled_fp8; needs 1.13 x the bound product <= 30); v is then only a shape
     reference. k_norm_slots (with prescaled, bf16): the float32 [64, 32] slots head_rmsnorm_rope(norm_max=...) filled
     for k, a data-tight key bound (cp25_attn_fwd_prescaled_kslots: blocks whose bound allows it run the zero-shift
-    loop even when norm_bounds do not)."""
+    loop even when norm_bounds do not).
+    q_norm=dict(weight=w [128] bf16, cos=None|[Lq, 64] fp32, sin=..., eps=1e-6, out_scale=c) (with prescaled, bf16
+    attention): q holds the raw projection and the kernel applies head_rmsnorm_rope(weight, cos, sin, out_scale)'s
+    arithmetic to its Q fragments as they load, bit for bit (cp25_attn_fwd_prescaled_qnorm): the separate q RMSNorm
+    pass over HBM is gone. cos / sin rows are indexed by the query row (token) of q."""
     lib = load_library()
     if q.dtype != torch.bfloat16 or k.dtype != torch.bfloat16 or v.dtype != torch.bfloat16:
         raise ValueError("attn_fwd expects bf16 q/k/v (attention() recasts to bf16 first)")
@@ -227,6 +233,8 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
     strides = [_i64x3((t.stride(0), t.stride(1), t.stride(2))) for t in (q, k, v, out)]
     if prescaled:
         if fp8_qk is not None:
+            if q_norm is not None:
+                raise ValueError("q_norm: the fp8 forms read e4m3 copies of the normalised q")
             if qb * kb > 60.0 or qb <= 0.0 or kb <= 0.0:
                 raise ValueError(f"fp8 Q K^T needs norm bounds with product <= 60, got {norm_bounds}")
             q8, k8 = fp8_qk
@@ -255,6 +263,24 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
         if k_norm_slots is not None:
             if k_norm_slots.dtype != torch.float32 or k_norm_slots.numel() != 2048 or not k_norm_slots.is_contiguous():
                 raise ValueError("k_norm_slots: a contiguous float32 [64, 32] slot buffer expected")
+        if q_norm is not None:
+            w, cos, sin = q_norm["weight"], q_norm.get("cos"), q_norm.get("sin")
+            if w.dtype != torch.bfloat16 or w.numel() != D or not w.is_contiguous() or w.device != q.device:
+                raise ValueError("q_norm: weight must be a contiguous bf16 [128] device tensor")
+            if (cos is None) != (sin is None):
+                raise ValueError("q_norm: cos and sin go together")
+            if cos is not None:
+                for t in (cos, sin):
+                    if t.dtype != torch.float32 or not t.is_contiguous() or t.dim() != 2 or t.shape[1] != 64 or \
+                            t.shape[0] < Lq or t.device != q.device:
+                        raise ValueError(f"q_norm: cos/sin must be contiguous float32 [>= {Lq}, 64] device tables")
+            rc = lib.cp25_attn_fwd_prescaled_qnorm(
+                _ptr(q), _ptr(k), _ptr(v), _ptr(out), B, H, Lq, Lk, D, *strides, qb, kb, _ptr(k_norm_slots),
+                64 if k_norm_slots is not None else 0, _ptr(w), _ptr(cos), _ptr(sin), float(q_norm.get("eps", 1e-6)),
+                float(q_norm.get("out_scale", 1.0)), int(n_split), _ptr(ws), ws_bytes, _stream(q.device))
+            _check("cp25_attn_fwd_prescaled_qnorm", rc)
+            return out
+        if k_norm_slots is not None:
             rc = lib.cp25_attn_fwd_prescaled_kslots(_ptr(q), _ptr(k), _ptr(v), _ptr(out), B, H, Lq, Lk, D, *strides, qb,
                                                     kb, _ptr(k_norm_slots), 64, int(n_split), _ptr(ws), ws_bytes,
                                                     _stream(q.device))
@@ -264,6 +290,8 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
                                          int(n_split), _ptr(ws), ws_bytes, _stream(q.device))
         _check("cp25_attn_fwd_prescaled", rc)
         return out
+    if q_norm is not None:
+        raise ValueError("q_norm needs prescaled=True (the DiT's attention form)")
     rc = lib.cp25_attn_fwd_bounded(
         _ptr(q), _ptr(k), _ptr(v), _ptr(out), B, H, Lq, Lk, D,
         _i64x3((q.stride(0), q.stride(1), q.stride(2))),

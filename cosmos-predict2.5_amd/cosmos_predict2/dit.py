@@ -228,6 +228,9 @@ class MinimalV1LVGDiT:
         # block or on the other CFG entry's keys, so context-parallel shards stay bit-identical to CP = 1 with any
         # checkpoint (tests/test_cp_gpu.py "nw_weight")
         self.data_tight_k_bound = False
+        # the self-attention normalises its own q (cp25_attn_fwd_prescaled_qnorm: head_rmsnorm_rope's arithmetic on
+        # the Q fragments as they load, bit-identical, no separate pass over q in HBM); prescaled bf16 form only
+        self.fused_q_norm = True
 
     def set_linear_precision(self, precision: str) -> None:
         """"bf16" (default, the reference's arithmetic) or "fp8": the 28 blocks' q/k/v, output, cross-q,
@@ -272,6 +275,10 @@ class MinimalV1LVGDiT:
         if self.attention_precision == "fp8" and 1.13 * qb * kb <= 30.0:
             kw["fp8_v"] = N.cast_v_fp8t(v)
         return kw
+
+    def _q_norm_in_attention(self, attn_kw: dict) -> bool:
+        """The self-attention launch applies the q RMSNorm + RoPE itself (fused_q_norm, prescaled bf16 form)."""
+        return self.fused_q_norm and attn_kw.get("prescaled", False) and self.attention_precision == "bf16"
 
     def _self_attn_mode(self, i: int, hd: int):
         """(q out_scale, attn_fwd kwargs) of block i's self-attention. q leaves the RMSNorm/RoPE kernel as
@@ -714,8 +721,13 @@ class MinimalV1LVGDiT:
                     qkv = self._proj(_rows(h, n * Bs), self.w_qkv[i], f"qkv.{i}")  # [n*Bs, 3D]
                     q_scale, attn_kw = self._self_attn_mode(i, hd)
                     kslots = self._k_slots(attn_kw)
-                    N.head_rmsnorm_rope(qkv, n_rows=n * Bs, B=Bs, H=H, head_off=0,
-                                        weight=p[pre + "self_attn.q_norm.weight"], cos=cos, sin=sin, out_scale=q_scale)
+                    if self._q_norm_in_attention(attn_kw):
+                        attn_kw = dict(attn_kw, q_norm=dict(weight=p[pre + "self_attn.q_norm.weight"], cos=cos, sin=sin,
+                                                            out_scale=q_scale))
+                    else:
+                        N.head_rmsnorm_rope(qkv, n_rows=n * Bs, B=Bs, H=H, head_off=0,
+                                            weight=p[pre + "self_attn.q_norm.weight"], cos=cos, sin=sin,
+                                            out_scale=q_scale)
                     N.head_rmsnorm_rope(qkv, n_rows=n * Bs, B=Bs, H=H, head_off=D,
                                         weight=p[pre + "self_attn.k_norm.weight"], cos=cos, sin=sin,
                                         **({} if kslots is None else dict(norm_max=kslots)))
@@ -832,8 +844,12 @@ class MinimalV1LVGDiT:
         work = all_gather_into_async(kv_all, kv, cp)  # RCCL over xGMI
         yield i  # the other lane's block runs here (in issue order) while this gather is in flight
         q_scale, attn_kw = self._self_attn_mode(i, hd)
-        N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=0, weight=p[pre + "self_attn.q_norm.weight"],
-                            cos=cos, sin=sin, out_scale=q_scale)
+        if self._q_norm_in_attention(attn_kw):
+            attn_kw = dict(attn_kw, q_norm=dict(weight=p[pre + "self_attn.q_norm.weight"], cos=cos, sin=sin,
+                                                out_scale=q_scale))
+        else:
+            N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=0, weight=p[pre + "self_attn.q_norm.weight"],
+                                cos=cos, sin=sin, out_scale=q_scale)
         w_ev = None
         if self.comm_events is not None:
             w_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))

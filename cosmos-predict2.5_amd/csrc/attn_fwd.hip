@@ -96,6 +96,14 @@ struct AttnArgs {
   float kbound;     // > 0: upper bound of |k| over all keys (fixed shift where it allows); 0: online max only
   const float* kslots;  // gated pair: max |k| over all keys = the max of n_kslots floats kslots[32 i] (device memory)
   int n_kslots;
+  // in-kernel q normalisation (cp25_attn_fwd_prescaled_qnorm, per-block forms): q holds the raw projection; each
+  // workgroup applies the per-head RMSNorm (weight qn_w[128], eps), the rotate-half RoPE of token qn_row0 + row
+  // (qn_cos / qn_sin [tokens][64] fp32; nullptr: none) and the factor qn_scale to its Q fragments as they load.
+  const unsigned short* qn_w;
+  const float* qn_cos;
+  const float* qn_sin;
+  float qn_eps, qn_scale;
+  int qn_row0;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -228,6 +236,69 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
     const unsigned short* src = qp + (int64_t)min(q_row[qh], a.Lq - 1) * a.q_sl + 8 * g;
 #pragma unroll
     for (int s = 0; s < 4; ++s) qf[qh][s] = *reinterpret_cast<const bf16x8*>(src + 32 * s);
+  }
+  if constexpr (!kPersist) {
+    if (a.qn_w != nullptr) {
+      // cp25_head_rmsnorm_rope on the fragments, operation for operation: the lane holds 8-element chunks
+      // 4 s + g (s = 0..3) of its rows, so that kernel's butterfly over 16 chunk lanes (xor 8, 4, 2, 1) is the
+      // in-lane pairs s ^ 2, s ^ 1, then lanes ^ 32 (g ^ 2) and ^ 16 (g ^ 1); RoPE pairs d with d ^ 64 = chunk s ^ 2
+      // every operand is requested before the first use of any (one exposed round trip, as without the norm; the
+      // loads in use order cost four in the prologue: +0.2 % per launch)
+      bf16x8 wv[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) wv[s] = *reinterpret_cast<const bf16x8*>(a.qn_w + 32 * s + 8 * g);
+      const bool rope = a.qn_cos != nullptr;
+      f32x4 rc[2][2][2], rsn[2][2][2];  // [qh][s & 1][half]: cos / sin of d mod 64 = 32 (s & 1) + 8 g + 4 half ..
+      if (rope) {
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) {
+          const int64_t t0 = (a.qn_row0 + min(q_row[qh], a.Lq - 1)) * 64 + 8 * g;
+#pragma unroll
+          for (int s1 = 0; s1 < 2; ++s1)
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+              rc[qh][s1][hf] = *reinterpret_cast<const f32x4*>(a.qn_cos + t0 + 32 * s1 + 4 * hf);
+              rsn[qh][s1][hf] = *reinterpret_cast<const f32x4*>(a.qn_sin + t0 + 32 * s1 + 4 * hf);
+            }
+        }
+      }
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) {
+        float x[4][8], p[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[s][e] = static_cast<float>(qf[qh][s][e]);
+          p[s] = hn_sumsq8(x[s]);
+        }
+        const float a0 = p[0] + p[2], a1 = p[1] + p[3];
+        float ss = a0 + a1;
+        ss += __shfl_xor(ss, 32);
+        ss += __shfl_xor(ss, 16);
+        const float rstd = hn_rstd(ss, a.qn_eps);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[s][e] = hn_norm(x[s][e], rstd, static_cast<float>(wv[s][e]));
+        if (rope) {
+          float y[4][8];
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              y[s][e] = hn_rope(x[s][e], x[s ^ 2][e], s < 2 ? -1.f : 1.f, rc[qh][s & 1][e >> 2][e & 3],
+                                rsn[qh][s & 1][e >> 2][e & 3]);
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x[s][e] = y[s][e];
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) qf[qh][s][e] = static_cast<__bf16>(x[s][e] * a.qn_scale);
+      }
+    }
   }
 
   if constexpr (kGate != 0) {
@@ -1281,7 +1352,8 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
                        const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
                        const int64_t* o_strides, float softmax_scale, float q_norm_bound, float k_norm_bound,
                        int n_split, void* workspace, size_t ws_bytes, hipStream_t stream, bool prescaled = false,
-                       int fp8 = 0, const float* v_amax = nullptr, const float* kslots = nullptr, int n_kslots = 0) {
+                       int fp8 = 0, const float* v_amax = nullptr, const float* kslots = nullptr, int n_kslots = 0,
+                       const AttnArgs* qn = nullptr) {
   const bool fp8qk = fp8 >= 1;
   if (D != kD) return CP25_ERR_DTYPE;
   if (fp8qk && !prescaled) return CP25_ERR_INVAL;
@@ -1346,6 +1418,12 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
   a.kbound = q_norm_bound > 0.f ? k_norm_bound : 0.f;  // a missing q bound: online (the kernel measures |q_row|)
   a.kslots = kslots;
   a.n_kslots = n_kslots;
+  a.qn_w = qn ? qn->qn_w : nullptr;
+  a.qn_cos = qn ? qn->qn_cos : nullptr;
+  a.qn_sin = qn ? qn->qn_sin : nullptr;
+  a.qn_eps = qn ? qn->qn_eps : 0.f;
+  a.qn_scale = qn ? qn->qn_scale : 1.f;
+  a.qn_row0 = 0;
   const int64_t nwg = (int64_t)a.nqb * B * H * n_split;
   if (nwg > 0x7fffffff) return CP25_ERR_INVAL;
   const bool xk = Lk <= 4096;  // short-key launches (text cross-attention) get their own symbol in profiles
@@ -1363,7 +1441,7 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
                          dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
       CP25_LAUNCH_CHECK();
       kern = xk ? attn_fwd_m16<1, true, 2, false, 2> : attn_fwd_m16<0, true, 2, false, 2>;
-    } else if (use_xattn_persistent(xk, n_split, mode, ntiles)) {
+    } else if (!qn && use_xattn_persistent(xk, n_split, mode, ntiles)) {  // (its Q path has no normalisation)
       // one workgroup per CU over contiguous runs of blocks (every workgroup gets at least one)
       grid = std::min<int64_t>(nwg, num_cus());
       if (prescaled) kern = mode == 2 ? attn_fwd_m16<1, true, 2, true> : attn_fwd_m16<1, true, 1, true>;
@@ -1393,6 +1471,7 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
       t.o = a.o + b * a.o_sb + h * a.o_sh + row0 * a.o_sl;
       t.B = 1; t.H = 1;
       t.Lq = (int)(std::min<int64_t>(Lq, row0 + (int64_t)g.nblk * kQBlk) - row0);
+      t.qn_row0 = (int)row0;  // the sub-problem's query row 0 is token row0 (RoPE tables)
       t.nqb = g.nblk;
       t.nsplit = g.s;
       t.tps = (int)cdiv(ntiles, g.s);
@@ -1495,6 +1574,29 @@ extern "C" int cp25_attn_fwd_prescaled_kslots(const void* q, const void* k, cons
   return attn_launch(q, k, v, o, B, H, Lq, Lk, D, q_strides, k_strides, v_strides, o_strides, 0.6931471805599453f,
                      q_norm_bound, k_norm_bound, n_split, workspace, ws_bytes, stream, true, 0, nullptr, k_norm_slots,
                      n_slots);
+}
+
+extern "C" int cp25_attn_fwd_prescaled_qnorm(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq,
+                                             int Lk, int D, const int64_t* q_strides, const int64_t* k_strides,
+                                             const int64_t* v_strides, const int64_t* o_strides, float q_norm_bound,
+                                             float k_norm_bound, const float* k_norm_slots, int n_slots,
+                                             const void* q_norm_weight, const float* cos_tab, const float* sin_tab,
+                                             float eps, float q_scale, int n_split, void* workspace, size_t ws_bytes,
+                                             hipStream_t stream) {
+  if (k_norm_slots && (n_slots < 1 || n_slots > 64 || ((uintptr_t)k_norm_slots & 3))) return CP25_ERR_INVAL;
+  if (!q_norm_weight || ((uintptr_t)q_norm_weight & 15) || (!cos_tab) != (!sin_tab) || !(eps >= 0.f) ||
+      !(q_scale > 0.f))
+    return CP25_ERR_INVAL;
+  if ((((uintptr_t)cos_tab) | ((uintptr_t)sin_tab)) & 3) return CP25_ERR_INVAL;
+  AttnArgs qn{};
+  qn.qn_w = (const unsigned short*)q_norm_weight;
+  qn.qn_cos = cos_tab;
+  qn.qn_sin = sin_tab;
+  qn.qn_eps = eps;
+  qn.qn_scale = q_scale;
+  return attn_launch(q, k, v, o, B, H, Lq, Lk, D, q_strides, k_strides, v_strides, o_strides, 0.6931471805599453f,
+                     q_norm_bound, k_norm_bound, n_split, workspace, ws_bytes, stream, true, 0, nullptr, k_norm_slots,
+                     k_norm_slots ? n_slots : 0, &qn);
 }
 
 extern "C" const char* cp25_attn_kernel(int Lk, float softmax_scale, float q_norm_bound, float k_norm_bound,

@@ -38,6 +38,30 @@ __device__ __forceinline__ unsigned short f2bf(float f) {
 // round an f32 to the nearest bf16 value and return it as f32 (emulates a bf16 tensor op)
 __device__ __forceinline__ float rbf(float f) { return bf2f(f2bf(f)); }
 
+// Per-head RMSNorm (TE, over 128 elements) + rotate-half RoPE, piece by piece: cp25_head_rmsnorm_rope's arithmetic,
+// shared by its kernel (dit_ops.hip) and the self-attention's in-kernel q normalisation (attn_fwd.hip), which reduce
+// the 16 8-element partial sums in the same order, so the two give the same bits. FP contraction off in each piece
+// (the attention's translation unit contracts by default).
+__device__ __forceinline__ float hn_sumsq8(const float* x) {  // x[0..7] sequentially
+#pragma clang fp contract(off)
+  float ss = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ss += x[e] * x[e];
+  return ss;
+}
+__device__ __forceinline__ float hn_rstd(float ss, float eps) {
+#pragma clang fp contract(off)
+  return rsqrtf(ss * (1.f / 128.f) + eps);
+}
+__device__ __forceinline__ float hn_norm(float x, float rstd, float w) {  // TE RMSNorm output -> bf16 value
+#pragma clang fp contract(off)
+  return rbf((x * rstd) * w);
+}
+__device__ __forceinline__ float hn_rope(float v, float partner, float sgn, float c, float s) {  // x cos + rot(x) sin
+#pragma clang fp contract(off)
+  return fmaf(v, c, (sgn * partner) * s);
+}
+
 // Exact-erf GELU, x * Phi(x) (minimal_v4_dit.py:249-254, nn.GELU()), with Phi from one erfc evaluation:
 // z = |x| / sqrt(2), erfc(z) = (1 + p(q)) / (1 + 2 z) * exp(-z^2), q = (z - 2) / (z + 2), p the degree-9 fit of
 // (1 + 2 z) exp(z^2) erfc(z) - 1 on z in [0, 10.5] (4.7e-8 relative; the construction of Juffa's erfcf), and

@@ -214,18 +214,15 @@ __global__ void __launch_bounds__(256) head_rmsnorm_rope_kernel(
   unsigned short* p = buf + row * row_stride + head_off + h * 128 + li * 8;
   u16x8 raw = *reinterpret_cast<const u16x8*>(p);
   float v[8];
-  float ss = 0.f;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    v[e] = bf2f(raw[e]);
-    ss += v[e] * v[e];
-  }
+  for (int e = 0; e < 8; ++e) v[e] = bf2f(raw[e]);
+  float ss = hn_sumsq8(v);  // (the reduction order attn_fwd.hip's in-kernel q normalisation repeats)
 #pragma unroll
   for (int m = 8; m >= 1; m >>= 1) ss += __shfl_xor(ss, m, 16);
-  const float rstd = rsqrtf(ss * (1.f / 128.f) + eps);
+  const float rstd = hn_rstd(ss, eps);
   u16x8 ww = *reinterpret_cast<const u16x8*>(w + li * 8);
 #pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = rbf((v[e] * rstd) * bf2f(ww[e]));  // TE RMSNorm -> bf16
+  for (int e = 0; e < 8; ++e) v[e] = hn_norm(v[e], rstd, bf2f(ww[e]));  // TE RMSNorm -> bf16
   if (cosb != nullptr) {
     // rotate-half RoPE in fp32 (TE fused rope, non-interleaved): y = x*cos + rot(x)*sin
     const int64_t tok = row / B;
@@ -238,7 +235,7 @@ __global__ void __launch_bounds__(256) head_rmsnorm_rope_kernel(
     for (int e = 0; e < 8; ++e) {
       const float c = cosb[tok * 64 + dlo + e];
       const float s = sinb[tok * 64 + dlo + e];
-      v[e] = fmaf(v[e], c, (sgn * partner[e]) * s);
+      v[e] = hn_rope(v[e], partner[e], sgn, c, s);
     }
   }
   u16x8 o;

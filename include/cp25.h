@@ -89,6 +89,22 @@ int cp25_attn_fwd_prescaled_kslots(const void* q, const void* k, const void* v, 
                                    const float* k_norm_slots, int n_slots, int n_split, void* workspace,
                                    size_t ws_bytes, hipStream_t stream);
 
+/* cp25_attn_fwd_prescaled (k_norm_slots NULL) / _kslots with the query normalisation done in the kernel: q holds the
+ * raw q projection (the QKV GEMM output) and every workgroup applies cp25_head_rmsnorm_rope's arithmetic to its Q
+ * fragments as they load: the per-head RMSNorm over 128 (q_norm_weight [128] bf16, eps), the rotate-half RoPE of
+ * the row's token (cos_tab / sin_tab [Lq][64] fp32, indexed by the query row; both NULL: none) and the factor
+ * q_scale (the softmax scale * log2 e of the prescaled form), with the same partial-sum order and roundings, so the
+ * output equals cp25_head_rmsnorm_rope_scaled followed by cp25_attn_fwd_prescaled bit for bit, without that
+ * pass over q in HBM (Attention.compute_qkv's q_norm + apply_rotary_pos_emb, minimal_v4_dit.py:401-419, then
+ * attention(), networks/attention.py:90-181). Per-block kernel forms only (a short-key launch that would take the
+ * persistent form runs one workgroup per query block instead). */
+int cp25_attn_fwd_prescaled_qnorm(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq, int Lk,
+                                  int D, const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
+                                  const int64_t* o_strides, float q_norm_bound, float k_norm_bound,
+                                  const float* k_norm_slots, int n_slots, const void* q_norm_weight,
+                                  const float* cos_tab, const float* sin_tab, float eps, float q_scale, int n_split,
+                                  void* workspace, size_t ws_bytes, hipStream_t stream);
+
 /* dst[r, c] = OCP e4m3(bf16 src[r, c] * scale) (saturated to +-448, round to nearest even), row strides in
  * elements; width % 16 == 0. The fixed-scale fp8 copies of q and k for cp25_attn_fwd_prescaled_fp8qk. */
 int cp25_cast_fp8_e4m3(const void* src, int64_t src_stride, void* dst, int64_t dst_stride, int64_t n_rows,

@@ -39,6 +39,9 @@ def main():
                     help="with --prescaled: Q K^T on e4m3 copies of q*4 and k/4 (cp25_attn_fwd_prescaled_fp8qk)")
     ap.add_argument("--fp8pv", action="store_true",
                     help="with --fp8qk: P.V on e5m2 P and e4m3 V too (cp25_attn_fwd_prescaled_fp8)")
+    ap.add_argument("--qnorm", action="store_true",
+                    help="with --bounded --prescaled: q stays the raw projection and the kernel applies the q RMSNorm "
+                         "+ RoPE + prescale itself (cp25_attn_fwd_prescaled_qnorm, the DiT's default since round 4)")
     ap.add_argument("--lib", default="", help="lab build of libcp25.so to load instead of the in-tree one")
     a = ap.parse_args()
     if a.lib:
@@ -59,6 +62,7 @@ def main():
         for t in (q, k, v):
             t.zero_()
     nb = None
+    q_raw = q.clone() if a.qnorm else None
     if a.bounded or a.normed:
         lo, hi = (float(x) for x in a.wrange.split(","))
         w = lo + (hi - lo) * torch.rand(128, device=dev, generator=torch.Generator(device=dev).manual_seed(5))
@@ -72,6 +76,12 @@ def main():
         q.copy_((q.float() * c).to(torch.bfloat16))
         nb = (nb[0] * c, nb[1]) if nb else None
         pre = dict(prescaled=True)
+        if a.qnorm:
+            assert a.bounded and not a.fp8qk, "--qnorm goes with --bounded --prescaled (bf16)"
+            ang = torch.rand(a.L, 64, device=dev, generator=torch.Generator(device=dev).manual_seed(6)) * 50.0
+            q.copy_(q_raw)
+            pre["q_norm"] = dict(weight=w.to(torch.bfloat16), cos=torch.cos(ang).contiguous(),
+                                 sin=torch.sin(ang).contiguous(), out_scale=c)
         if a.fp8qk:
             if a.fused:
                 cols = [buf.view(a.L * a.B, 3 * D)[:, i * D:(i + 1) * D] for i in range(2)]
@@ -105,7 +115,7 @@ def main():
     ms = e0.elapsed_time(e1) / a.iters
     flop = 4.0 * a.B * a.H * a.L * Lk * 128
     print(json.dumps({"kernel": "attn_fwd", "B": a.B, "H": a.H, "Lq": a.L, "Lk": Lk, "fused": a.fused,
-                      "zeros": a.zeros, "bounded": a.bounded, "prescaled": a.prescaled, "fp8qk": a.fp8qk, "fp8pv": a.fp8pv, "normed": a.normed or a.bounded, "wrange": a.wrange, "split": ns or N.attn_plan(a.B, a.H, a.L, Lk), "iters": a.iters, "lib": os.path.basename(a.lib) or "libcp25.so", "ms": ms,
+                      "zeros": a.zeros, "bounded": a.bounded, "prescaled": a.prescaled, "fp8qk": a.fp8qk, "fp8pv": a.fp8pv, "qnorm": a.qnorm, "normed": a.normed or a.bounded, "wrange": a.wrange, "split": ns or N.attn_plan(a.B, a.H, a.L, Lk), "iters": a.iters, "lib": os.path.basename(a.lib) or "libcp25.so", "ms": ms,
                       "tflops": flop / ms / 1e9, "check_rel_l2": check}))
 
 
