@@ -188,7 +188,9 @@ constexpr int kLdsP = kLds16 + kWaves * kQSlot;     // 141312
 // whose query block's bound max|q_row| max|k| is <= 96 runs in the first launch (no shift, the fast loop) and exits
 // at once in the second, any other runs in the second (online max). Each block's arithmetic is exactly that of its
 // mode; which mode a row gets depends on the other rows of its 256-row block.
-template <int kKind, bool kPre, int kMode, bool kPersist = false, int kGate = 0>
+// kTail = 1: the same code as a separate symbol, launched for the tail-split segments, so profiles separate the main
+// grid from the segments that finish its last partial round.
+template <int kKind, bool kPre, int kMode, bool kPersist = false, int kGate = 0, int kTail = 0>
 __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[kPersist ? kLdsP : kLds16];
   constexpr int KB1 = kKBuf16, VB0 = 2 * kKBuf16;
@@ -1434,6 +1436,7 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
   } else {
     const int mode = m16_mode(q_norm_bound, k_norm_bound, a.scale_log2, prescaled);
     void (*kern)(AttnArgs) = nullptr;
+    void (*kern_tail)(AttnArgs) = nullptr;  // the tail segments' symbol (plan_tail: self-attention shapes only)
     int64_t grid = nwg;
     if (prescaled && kslots && mode != 1) {
       // the gated pair: blocks whose data-tight bound allows it run the zero-shift loop, the others the online max
@@ -1447,11 +1450,12 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
       if (prescaled) kern = mode == 2 ? attn_fwd_m16<1, true, 2, true> : attn_fwd_m16<1, true, 1, true>;
       else kern = attn_fwd_m16<1, false, 2, true>;
     } else {
-#define M16(P, M) kern = xk ? attn_fwd_m16<1, P, M> : attn_fwd_m16<0, P, M>
+#define M16(P, M) kern = xk ? attn_fwd_m16<1, P, M> : attn_fwd_m16<0, P, M>; \
+                  kern_tail = attn_fwd_m16<0, P, M, false, 0, 1>
       if (prescaled) {
-        if (mode == 2) M16(true, 2); else if (mode == 1) M16(true, 1); else M16(true, 0);
+        if (mode == 2) { M16(true, 2); } else if (mode == 1) { M16(true, 1); } else { M16(true, 0); }
       } else {
-        if (mode == 2) M16(false, 2); else M16(false, 0);
+        if (mode == 2) { M16(false, 2); } else { M16(false, 0); }
       }
 #undef M16
       if (n_tail) grid = nwg - nwg % num_cus();  // whole rounds; the rest below
@@ -1477,7 +1481,7 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
       t.tps = (int)cdiv(ntiles, g.s);
       t.o_part = (float*)workspace;
       t.lse_part = (float*)workspace + (size_t)g.s * t.Lq * kD;
-      hipLaunchKernelGGL(kern, dim3((unsigned)(g.nblk * g.s)), dim3(kThreads), 0, stream, t);
+      hipLaunchKernelGGL(kern_tail, dim3((unsigned)(g.nblk * g.s)), dim3(kThreads), 0, stream, t);
       CP25_LAUNCH_CHECK();
       hipLaunchKernelGGL(attn_merge_splits, dim3((unsigned)cdiv((int64_t)t.Lq * 32, 256)), dim3(256), 0, stream,
                          t.o_part, t.lse_part, t.o, g.s, 1, 1, t.Lq, a.o_sb, a.o_sl, a.o_sh);

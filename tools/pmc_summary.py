@@ -1,4 +1,4 @@
-"""Summarise tools/pmc_attn.sh / tools/pmc_passes.sh passes for one kernel (its last, i.e. timed, dispatch).
+"""Summarise tools/pmc_attn.sh / tools/pmc_passes.sh passes for one kernel (its longest, i.e. timed, dispatch).
 
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) is doubled on gfx950 for 16-B/lane
 streaming reads; WRITE_SIZE (KiB) is exact for 16-B streaming stores. Prints one JSON object.
@@ -30,7 +30,8 @@ def load(out, kernels=KERNELS):
             per[d][r["Counter_Name"]] += float(r["Counter_Value"])
             span[d] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         if per:
-            last = max(per)
+            # the longest dispatch: the timed launch (tail-split segments and small correctness launches share names)
+            last = max(per, key=lambda d: span[d])
             vals.update(per[last])
             dur[os.path.basename(f)] = span[last]
     return vals, dur
