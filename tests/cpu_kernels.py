@@ -74,10 +74,16 @@ def copy_rows(src, src_stride, dst, dst_stride, n_rows, width, src_offset=0):
 
 
 def attn_fwd(q, k, v, out=None, softmax_scale=None, n_split=None, norm_bounds=None, prescaled=False, fp8_qk=None,
-             fp8_v=None):
+             fp8_v=None, k_norm_slots=None, q_norm=None):
     if fp8_qk is not None or fp8_v is not None:
         raise NotImplementedError
     D = q.shape[-1]
+    if q_norm is not None:  # the in-kernel q normalisation: head_rmsnorm_rope's arithmetic on a copy of q
+        Bq, Lq, H = q.shape[:3]
+        qq = q.transpose(0, 1).contiguous().view(Lq * Bq, H * D)
+        head_rmsnorm_rope(qq, n_rows=Lq * Bq, B=Bq, H=H, head_off=0, weight=q_norm["weight"], cos=q_norm.get("cos"),
+                          sin=q_norm.get("sin"), eps=q_norm.get("eps", 1e-6), out_scale=q_norm.get("out_scale", 1.0))
+        q = qq.view(Lq, Bq, H, D).transpose(0, 1)
     c = math.log(2.0) if prescaled else (D ** -0.5 if softmax_scale is None else softmax_scale)
     s = torch.einsum("blhd,bmhd->bhlm", q.float(), k.float()) * c
     o = torch.einsum("bhlm,bmhd->blhd", torch.softmax(s, -1), v.float()).to(BF16)

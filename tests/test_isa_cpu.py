@@ -31,12 +31,14 @@ def test_no_lds_read_races(src):
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="hipcc not installed")
 def test_self_attention_loop_shape():
-    rep = isa_check.check(os.path.join(CSRC, "attn_fwd.hip"), "attn_fwd_m16ILi0ELb1ELi1ELb0ELi0E")
+    rep = isa_check.check(os.path.join(CSRC, "attn_fwd.hip"), "attn_fwd_m16ILi0ELb1ELi1ELb0ELi0ELi0EE")
     (r,) = rep.values()  # the bench's kernel: self-attention, prescaled q, zero shift
     # scratch traffic only in the loop's cold contract-guard branch (a NaN poison of overflowed rows), never in the
     # MFMA / softmax phases: at most the one reload + one spill of the NaN fill
     assert r["inloop_scratch"] <= 2, r["inloop_scratch"]
-    assert r["nops"] <= 40, r["nops"]  # 192 with the operand-redefining wait pins
+    # 192 with the operand-redefining wait pins; the prologue's in-kernel q normalisation adds 2 per rsqrt (two rows per
+    # lane: v_cmp -> v_cndmask and v_rsq pads, outside the loop)
+    assert r["nops"] <= 44, r["nops"]
 
 
 _SYNTH = """_Zk:
