@@ -80,6 +80,7 @@ SIGNATURES = {
     "cp25_copy_rows": [_P, _I64, _P, _I64, _I64, _I64, _P],
     "cp25_gelu": [_P, _I64, _P],
     "cp25_gemm_epi": [_P, _I64, _P, _I64, _P, _I64, _I, _I, _I, _I, _P],
+    "cp25_gemm_hnorm": [_P, _I64, _P, _I64, _P, _I64, _I, _I, _I, _P, _F, _F, _P],
     "cp25_gemm_res": [_P, _I64, _P, _I64, _P, _I64, _I, _I, _I, _P, _I64, _I64, _P, _I64, _I64, _I, _I64, _I64, _P],
     "cp25_gemm_fp8": [_P, _I64, _P, _P, _I64, _P, _P, _I64, _I, _I, _I, _P],
     "cp25_gemm_fp8_res": [_P, _I64, _P, _P, _I64, _P, _P, _I64, _I, _I, _I, _P, _I64, _I64, _P, _I64, _I64, _I, _I64,
@@ -456,7 +457,7 @@ def gelu_(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
-EPI_NONE, EPI_GELU, EPI_RES = 0, 1, 2
+EPI_NONE, EPI_GELU, EPI_RES, EPI_HNORM = 0, 1, 2, 3
 
 
 def gemm_supported(N: int, K: int) -> bool:
@@ -487,6 +488,32 @@ def gemm_epi(a: torch.Tensor, w: torch.Tensor, epilogue: int = EPI_NONE, out: Op
     rc = lib.cp25_gemm_epi(_ptr(a), a.stride(0), _ptr(w), w.stride(0), _ptr(out), out.stride(0), M, N, K, int(epilogue),
                            _stream(a.device))
     _check("cp25_gemm_epi", rc)
+    return out
+
+
+def gemm_hnorm(a: torch.Tensor, w: torch.Tensor, norm_weight: torch.Tensor, *, out_scale: float = 1.0,
+               eps: float = 1e-6, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """out[M, N] = per-128-column-head RMSNorm(bf16(a w^T)) * norm_weight * out_scale (cp25_gemm_hnorm), bit-identical
+    to gemm_epi followed by head_rmsnorm_rope(out_scale=...) without RoPE (the cross-attention q projection + q_norm).
+    None when the kernel is not built for the shape (K / 64 odd): the caller runs the two ops."""
+    lib = load_library()
+    if a.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or norm_weight.dtype != torch.bfloat16:
+        raise ValueError("gemm_hnorm expects bf16 operands and norm weight")
+    if a.dim() != 2 or w.dim() != 2 or a.shape[1] != w.shape[1] or a.stride(1) != 1 or w.stride(1) != 1:
+        raise ValueError(f"gemm_hnorm shapes a{tuple(a.shape)} w{tuple(w.shape)}: need [M, K] x [N, K], K contiguous")
+    if norm_weight.numel() != 128 or not norm_weight.is_contiguous() or norm_weight.device != a.device:
+        raise ValueError("gemm_hnorm: norm_weight must be a contiguous bf16 [128] device tensor")
+    M, K = a.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    if tuple(out.shape) != (M, N) or out.stride(1) != 1:
+        raise ValueError(f"gemm_hnorm out {tuple(out.shape)} != ({M}, {N})")
+    rc = lib.cp25_gemm_hnorm(_ptr(a), a.stride(0), _ptr(w), w.stride(0), _ptr(out), out.stride(0), M, N, K,
+                             _ptr(norm_weight), float(eps), float(out_scale), _stream(a.device))
+    if rc == -95:
+        return None
+    _check("cp25_gemm_hnorm", rc)
     return out
 
 

@@ -761,10 +761,15 @@ class MinimalV1LVGDiT:
             if prefix_only:
                 return x, h
             # ---- cross attention (a shared query is read with batch stride 0 against each entry's text K/V)
-            qc = self._proj(_rows(h, n * Bs), p[pre + "cross_attn.q_proj.weight"], pre + "cross_attn.q_proj")
             xq_scale, xattn_kw = self._attn_mode(self.xattn_bounds[i], hd)  # prescaled q as in self-attention
-            N.head_rmsnorm_rope(qc, n_rows=n * Bs, B=Bs, H=H, head_off=0, weight=p[pre + "cross_attn.q_norm.weight"],
-                                out_scale=xq_scale)
+            hq, wq = _rows(h, n * Bs), p[pre + "cross_attn.q_proj.weight"]
+            qc = None
+            if self._own(hq, wq):  # the q RMSNorm (+ prescale) in the GEMM's epilogue (cp25_gemm_hnorm, bit-identical)
+                qc = N.gemm_hnorm(hq, wq, p[pre + "cross_attn.q_norm.weight"], out_scale=xq_scale)
+            if qc is None:
+                qc = self._proj(hq, wq, pre + "cross_attn.q_proj")
+                N.head_rmsnorm_rope(qc, n_rows=n * Bs, B=Bs, H=H, head_off=0,
+                                    weight=p[pre + "cross_attn.q_norm.weight"], out_scale=xq_scale)
             o = torch.empty((n, B, D), dtype=BF16, device=self.device)
             self._cross_attention(qc.view(n, Bs, H, hd).expand(n, B, H, hd), ctx.k[i], ctx.v[i], o.view(n, B, H, hd),
                                   geo, xattn_kw)

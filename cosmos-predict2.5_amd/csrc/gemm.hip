@@ -15,6 +15,10 @@
 //                                     token-major row (tok, b) = (row / B, row % B) and the row's frame
 //                                     (tok0 + tok) / hw; the next LN-mod then reads the new x once instead of x
 //                                     and y (cp25_ln_mod with y = NULL).
+//                     CP25_EPI_HNORM: C = bf16(bf16(RMSNorm_head(bf16(acc)) * w) * out_scale) per 128-column head,
+//                                     the cross-attention q projection + its q_norm (:401-404, :411-419 without
+//                                     RoPE) with cp25_head_rmsnorm_rope's partial sums, butterfly and roundings
+//                                     (cp25_common.h hn_*): bit-identical to the GEMM followed by that kernel.
 //
 // Design (MI355X, see DESIGN.md §3 "GEMM"): 256 x 256 output tile per 512-thread workgroup (one per
 // CU), 8 waves as 2 (M) x 4 (N), each wave 128 x 64 with v_mfma_f32_16x16x32_bf16 (32 accumulators,
@@ -57,10 +61,13 @@ __device__ __forceinline__ float gelu_exact(float a) { return gelu_erf(a); }  //
 
 // CP25_EPI_RES operands: output row r = token (r / B) batch entry (r % B); x element (tok, b, col) at
 // tok * x_st + b * x_sb + col, gate element (b, frame, col) at b * g_sb + frame * g_st + col, frame = (tok0 + tok) / hw
+// CP25_EPI_HNORM (the cross-attention's q projection, cp25_gemm_hnorm): per-head RMSNorm of the bf16 product with
+// weight nw[128], eps, then x out_scale, the arithmetic of cp25_head_rmsnorm_rope without RoPE
 struct ResEpi {
   const unsigned short* x; int64_t x_st, x_sb;
   const unsigned short* gate; int64_t g_sb, g_st;
   int B; int64_t tok0, hw;
+  const unsigned short* nw; float n_eps, n_scale;
 };
 
 // x + gate * y on 8 bf16 columns, two bf16 roundings (the reference's two torch ops, = cp25_ln_mod's residual)
@@ -411,6 +418,8 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
 
   int tile = my_slot;
   if (tile >= n_tiles) return;
+  u32x4 nwv = {0u, 0u, 0u, 0u};  // CP25_EPI_HNORM: this lane's 8 norm weights (columns 8 (ch & 15) .. of its head)
+  if constexpr (kEpi == CP25_EPI_HNORM) nwv = *reinterpret_cast<const u32x4*>(re.nw + (tid & 15) * 8);
   if constexpr (kEpi == CP25_EPI_GELU) {  // the GELU table (visible after the prologue's barrier)
     unsigned short* tab = reinterpret_cast<unsigned short*>(smem + 2 * kBuf8);
     for (int i = tid; i < kGeluTab; i += kThreads) {
@@ -566,6 +575,31 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
       issue_first_two();
     }
     __builtin_amdgcn_sched_barrier(0);  // the DMAs are queued ahead of the stores (the counts above rely on it)
+    if constexpr (kEpi == CP25_EPI_HNORM) {
+      // lanes 16 h .. 16 h + 15 of a 32-lane row hold head h's 128 columns, lane li = ch & 15 the 8 columns 8 li ..:
+      // cp25_head_rmsnorm_rope's item layout, so its butterfly over 16 lanes is this one (runs under the DMA above)
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        float v[8];
+#pragma unroll
+        for (int w2 = 0; w2 < 4; ++w2) {
+          v[2 * w2] = bf2f((unsigned short)(cv[it][w2] & 0xffffu));
+          v[2 * w2 + 1] = bf2f((unsigned short)(cv[it][w2] >> 16));
+        }
+        float ss = hn_sumsq8(v);
+#pragma unroll
+        for (int m = 8; m >= 1; m >>= 1) ss += __shfl_xor(ss, m, 16);
+        const float rstd = hn_rstd(ss, re.n_eps);
+        u32x4 o;
+#pragma unroll
+        for (int w2 = 0; w2 < 4; ++w2) {
+          const float lo = hn_norm(v[2 * w2], rstd, bf2f((unsigned short)(nwv[w2] & 0xffffu)));
+          const float hi = hn_norm(v[2 * w2 + 1], rstd, bf2f((unsigned short)(nwv[w2] >> 16)));
+          o[w2] = (unsigned)f2bf(lo * re.n_scale) | ((unsigned)f2bf(hi * re.n_scale) << 16);
+        }
+        cv[it] = o;
+      }
+    }
     if (full) {
 #pragma unroll
       for (int it = 0; it < 16; ++it) *reinterpret_cast<u32x4*>(crow + (int64_t)it * 16 * ldc) = cv[it];
@@ -593,7 +627,12 @@ static int gemm_launch(const void* a, int64_t lda, const void* w, int64_t ldw, v
   if (lda < K || ldw < K || ldc < N || (lda % 8) || (ldw % 8) || (ldc % 8)) return CP25_ERR_INVAL;
   if (lda >= (1 << 22) || ldw >= (1 << 22)) return CP25_ERR_INVAL;  // 32-bit in-tile byte offsets
   if (((uintptr_t)a | (uintptr_t)w | (uintptr_t)c) & 15) return CP25_ERR_INVAL;
-  if (epilogue != CP25_EPI_NONE && epilogue != CP25_EPI_GELU && epilogue != CP25_EPI_RES) return CP25_ERR_INVAL;
+  if (epilogue != CP25_EPI_NONE && epilogue != CP25_EPI_GELU && epilogue != CP25_EPI_RES && epilogue != CP25_EPI_HNORM)
+    return CP25_ERR_INVAL;
+  if (epilogue == CP25_EPI_HNORM) {
+    if (!re.nw || ((uintptr_t)re.nw & 15) || !(re.n_eps >= 0.f) || !(re.n_scale > 0.f)) return CP25_ERR_INVAL;
+    if ((K / kBK) % 2 != 0) return CP25_ERR_DTYPE;  // the persistent kernel only (the caller runs the separate norm)
+  }
   if (epilogue == CP25_EPI_RES) {
     if (!re.x || !re.gate || re.B <= 0 || 16 % re.B || re.hw < 16 / re.B || re.tok0 < 0 || (re.x_st % 8) || (re.x_sb % 8) ||
         (re.g_sb % 8) || (re.g_st % 8) || (((uintptr_t)re.x | (uintptr_t)re.gate) & 15))
@@ -633,6 +672,10 @@ static int gemm_launch(const void* a, int64_t lda, const void* w, int64_t ldw, v
       case CP25_EPI_RES:
         hipLaunchKernelGGL((gemm_nt_8ph<CP25_EPI_RES, 2>), pgrid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re,
                            nullptr, nullptr);
+        break;
+      case CP25_EPI_HNORM:
+        hipLaunchKernelGGL((gemm_nt_8ph<CP25_EPI_HNORM, 2>), pgrid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K,
+                           re, nullptr, nullptr);
         break;
       default:
         hipLaunchKernelGGL((gemm_nt_8ph<CP25_EPI_NONE, 2>), pgrid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re,
@@ -693,9 +736,18 @@ extern "C" int cp25_gemm_fp8_res(const void* a, int64_t lda, const float* a_scal
   return gemm_fp8_launch(a, lda, a_scale, w, ldw, w_scale, c, ldc, M, N, K, CP25_EPI_RES, re, stream);
 }
 
+extern "C" int cp25_gemm_hnorm(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int M,
+                               int N, int K, const void* norm_weight, float eps, float out_scale, hipStream_t stream) {
+  ResEpi re{};
+  re.nw = (const unsigned short*)norm_weight;
+  re.n_eps = eps;
+  re.n_scale = out_scale;
+  return gemm_launch(a, lda, w, ldw, c, ldc, M, N, K, CP25_EPI_HNORM, re, stream);
+}
+
 extern "C" int cp25_gemm_epi(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int M,
                              int N, int K, int epilogue, hipStream_t stream) {
-  if (epilogue == CP25_EPI_RES) return CP25_ERR_INVAL;  // needs its operands: cp25_gemm_res
+  if (epilogue == CP25_EPI_RES || epilogue == CP25_EPI_HNORM) return CP25_ERR_INVAL;  // their operands: _res / _hnorm
   const ResEpi re{};
   return gemm_launch(a, lda, w, ldw, c, ldc, M, N, K, epilogue, re, stream);
 }

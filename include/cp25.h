@@ -246,8 +246,18 @@ int cp25_gelu(void* x, int64_t n, hipStream_t stream);
 #define CP25_EPI_NONE 0
 #define CP25_EPI_GELU 1
 #define CP25_EPI_RES 2
+#define CP25_EPI_HNORM 3
 int cp25_gemm_epi(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int M, int N, int K,
                   int epilogue, hipStream_t stream);
+
+/* cp25_gemm_epi with the per-head q RMSNorm as the epilogue (CP25_EPI_HNORM): every 128-column head of each output row
+ * of bf16(A W^T) normalised over its 128 values (norm_weight [128] bf16, eps) and multiplied by out_scale, with the
+ * partial sums, butterfly and roundings of cp25_head_rmsnorm_rope (no RoPE): bit-identical to cp25_gemm_epi followed
+ * by cp25_head_rmsnorm_rope_scaled on the output, one HBM pass fewer. Replaces the cross-attention's q_proj + q_norm
+ * (minimal_v4_dit.py:401-404, :411-419; the text cross-attention has no RoPE). K / 64 must be even (else
+ * CP25_ERR_DTYPE: run the two ops). */
+int cp25_gemm_hnorm(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int M, int N, int K,
+                    const void* norm_weight, float eps, float out_scale, hipStream_t stream);
 
 /* cp25_gemm_epi with the block's gated residual as the epilogue: C = bf16(x + bf16(gate * bf16(A W^T))), the two
  * bf16 roundings of the reference's `x + gate * y` (cp25_ln_mod's residual, bit for bit). Output row r is token

@@ -157,6 +157,16 @@ def rms_norm_silu(x, gamma, silu=True, out=None):
     return out
 
 
+def gemm_hnorm(a, w, norm_weight, *, out_scale=1.0, eps=1e-6, out=None):
+    y = F.linear(a, w)
+    head_rmsnorm_rope(y, n_rows=y.shape[0], B=1, H=y.shape[1] // 128, head_off=0, weight=norm_weight, eps=eps,
+                      out_scale=out_scale)
+    if out is None:
+        return y
+    out.copy_(y)
+    return out
+
+
 def vae_attn(q, k, v, out=None, scale=None):
     sc = q.shape[-1] ** -0.5 if scale is None else scale
     p = torch.softmax(torch.einsum("tld,tmd->tlm", q.double(), k.double()) * sc, -1)
@@ -168,7 +178,8 @@ def vae_attn(q, k, v, out=None, scale=None):
 
 
 _FUNCS = dict(conv3d=conv3d, rms_norm_silu=rms_norm_silu, vae_attn=vae_attn, ln_mod=ln_mod, final_ln_mod=final_ln_mod, head_rmsnorm_rope=head_rmsnorm_rope, copy_rows=copy_rows,
-              attn_fwd=attn_fwd, attn_kernel_name=attn_kernel_name, gemm_epi=gemm_epi, gemm_res=gemm_res, gelu_=gelu_)
+              attn_fwd=attn_fwd, attn_kernel_name=attn_kernel_name, gemm_epi=gemm_epi, gemm_res=gemm_res,
+              gemm_hnorm=gemm_hnorm, gelu_=gelu_)
 
 
 @contextlib.contextmanager
