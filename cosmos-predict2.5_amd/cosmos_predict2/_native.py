@@ -81,6 +81,7 @@ SIGNATURES = {
     "cp25_gelu": [_P, _I64, _P],
     "cp25_gemm_epi": [_P, _I64, _P, _I64, _P, _I64, _I, _I, _I, _I, _P],
     "cp25_gemm_hnorm": [_P, _I64, _P, _I64, _P, _I64, _I, _I, _I, _P, _F, _F, _P],
+    "cp25_gemm_qkv": [_P, _I64, _P, _I64, _P, _I64, _I, _I, _I, _I, _I, _P, _P, _P, _I, _F, _P],
     "cp25_gemm_res": [_P, _I64, _P, _I64, _P, _I64, _I, _I, _I, _P, _I64, _I64, _P, _I64, _I64, _I, _I64, _I64, _P],
     "cp25_gemm_fp8": [_P, _I64, _P, _P, _I64, _P, _P, _I64, _I, _I, _I, _P],
     "cp25_gemm_fp8_res": [_P, _I64, _P, _P, _I64, _P, _P, _I64, _I, _I, _I, _P, _I64, _I64, _P, _I64, _I64, _I, _I64,
@@ -457,7 +458,7 @@ def gelu_(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
-EPI_NONE, EPI_GELU, EPI_RES, EPI_HNORM = 0, 1, 2, 3
+EPI_NONE, EPI_GELU, EPI_RES, EPI_HNORM, EPI_QKV = 0, 1, 2, 3, 4
 
 
 def gemm_supported(N: int, K: int) -> bool:
@@ -514,6 +515,42 @@ def gemm_hnorm(a: torch.Tensor, w: torch.Tensor, norm_weight: torch.Tensor, *, o
     if rc == -95:
         return None
     _check("cp25_gemm_hnorm", rc)
+    return out
+
+
+def gemm_qkv(a: torch.Tensor, w: torch.Tensor, k_norm_weight: torch.Tensor, *, k_col0: int, k_cols: int, B: int,
+             cos: Optional[torch.Tensor] = None, sin: Optional[torch.Tensor] = None, eps: float = 1e-6,
+             out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """The fused q|k|v projection out[M, N] = bf16(a w^T) with the k columns [k_col0, k_col0 + k_cols) normalised per
+    128-column head (k_norm_weight, eps) and rotated by the RoPE of token row // B (cos / sin [M / B, 64] fp32 or None)
+    in the epilogue (cp25_gemm_qkv): bit-identical to gemm_epi + head_rmsnorm_rope on those columns. None when the
+    kernel is not built for the shape (K / 64 odd): the caller runs the two ops."""
+    lib = load_library()
+    if a.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or k_norm_weight.dtype != torch.bfloat16:
+        raise ValueError("gemm_qkv expects bf16 operands and norm weight")
+    if a.dim() != 2 or w.dim() != 2 or a.shape[1] != w.shape[1] or a.stride(1) != 1 or w.stride(1) != 1:
+        raise ValueError(f"gemm_qkv shapes a{tuple(a.shape)} w{tuple(w.shape)}: need [M, K] x [N, K], K contiguous")
+    if k_norm_weight.numel() != 128 or not k_norm_weight.is_contiguous() or k_norm_weight.device != a.device:
+        raise ValueError("gemm_qkv: k_norm_weight must be a contiguous bf16 [128] device tensor")
+    M, K = a.shape
+    N = w.shape[0]
+    if (cos is None) != (sin is None):
+        raise ValueError("gemm_qkv: cos and sin go together")
+    if cos is not None:
+        for t in (cos, sin):
+            if t.dtype != torch.float32 or not t.is_contiguous() or t.dim() != 2 or t.shape[1] != 64 or \
+                    t.shape[0] * B < M or t.device != a.device:
+                raise ValueError(f"gemm_qkv: cos/sin must be contiguous float32 [>= {M // B}, 64] device tables")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    if tuple(out.shape) != (M, N) or out.stride(1) != 1:
+        raise ValueError(f"gemm_qkv out {tuple(out.shape)} != ({M}, {N})")
+    rc = lib.cp25_gemm_qkv(_ptr(a), a.stride(0), _ptr(w), w.stride(0), _ptr(out), out.stride(0), M, N, K, int(k_col0),
+                           int(k_cols), _ptr(k_norm_weight), _ptr(cos), _ptr(sin), int(B), float(eps),
+                           _stream(a.device))
+    if rc == -95:
+        return None
+    _check("cp25_gemm_qkv", rc)
     return out
 
 

@@ -343,6 +343,22 @@ class MinimalV1LVGDiT:
         """A block projection without epilogue (QKV, cross-attention q)."""
         return N.gemm_epi(x, w) if self._own(x, w) else self._linear(x, w, key)
 
+    def _qkv_k_normed(self, h, i: int, n_rows: int, B: int, cos, sin, kslots=None) -> torch.Tensor:
+        """Block i's fused q|k|v projection [n_rows, 3D] with k RMSNorm'd + RoPE'd: in the own GEMM's epilogue
+        (cp25_gemm_qkv, bit-identical) where it applies, else the projection and the k pass of cp25_head_rmsnorm_rope
+        (which also fills the data-tight key-bound slots when kslots is given)."""
+        cfg = self.cfg
+        D, H = cfg.model_channels, cfg.num_heads
+        x, w, kw = _rows(h, n_rows), self.w_qkv[i], self.sd[f"blocks.{i}.self_attn.k_norm.weight"]
+        if kslots is None and self._own(x, w):
+            qkv = N.gemm_qkv(x, w, kw, k_col0=D, k_cols=D, B=B, cos=cos, sin=sin)
+            if qkv is not None:
+                return qkv
+        qkv = self._proj(x, w, f"qkv.{i}")
+        N.head_rmsnorm_rope(qkv, n_rows=n_rows, B=B, H=H, head_off=D, weight=kw, cos=cos, sin=sin,
+                            **({} if kslots is None else dict(norm_max=kslots)))
+        return qkv
+
     def _proj_res(self, a, w: torch.Tensor, key: str, x: torch.Tensor, x_st: int, x_sb: int, gate: torch.Tensor,
                   B: int, geo: "Geometry", n: int, lnk: dict, shift=None, scale=None, gelu_in: bool = False):
         """x' = x + gate * (a w^T) (Block.forward's gated residuals, minimal_v4_dit.py:1204, 1237, 1246) for the token-
@@ -718,9 +734,9 @@ class MinimalV1LVGDiT:
                 if self.attn_events is not None:
                     ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 if cp is None or cp_size == 1:
-                    qkv = self._proj(_rows(h, n * Bs), self.w_qkv[i], f"qkv.{i}")  # [n*Bs, 3D]
                     q_scale, attn_kw = self._self_attn_mode(i, hd)
                     kslots = self._k_slots(attn_kw)
+                    qkv = self._qkv_k_normed(h, i, n * Bs, Bs, cos, sin, kslots)  # [n*Bs, 3D], k normed + roped
                     if self._q_norm_in_attention(attn_kw):
                         attn_kw = dict(attn_kw, q_norm=dict(weight=p[pre + "self_attn.q_norm.weight"], cos=cos, sin=sin,
                                                             out_scale=q_scale))
@@ -728,9 +744,6 @@ class MinimalV1LVGDiT:
                         N.head_rmsnorm_rope(qkv, n_rows=n * Bs, B=Bs, H=H, head_off=0,
                                             weight=p[pre + "self_attn.q_norm.weight"], cos=cos, sin=sin,
                                             out_scale=q_scale)
-                    N.head_rmsnorm_rope(qkv, n_rows=n * Bs, B=Bs, H=H, head_off=D,
-                                        weight=p[pre + "self_attn.k_norm.weight"], cos=cos, sin=sin,
-                                        **({} if kslots is None else dict(norm_max=kslots)))
                     if kslots is not None:
                         attn_kw = dict(attn_kw, k_norm_slots=kslots)
                     q = qkv.view(n, Bs, 3 * D)[:, :, :D].view(n, Bs, H, hd).transpose(0, 1)
@@ -840,9 +853,7 @@ class MinimalV1LVGDiT:
         p = self.sd
         pre = f"blocks.{i}."
         D, H, hd = cfg.model_channels, cfg.num_heads, cfg.head_dim
-        qkv = self._proj(_rows(h, n * B), self.w_qkv[i], f"qkv.{i}")  # [n*B, 3D]
-        N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=D, weight=p[pre + "self_attn.k_norm.weight"],
-                            cos=cos, sin=sin)
+        qkv = self._qkv_k_normed(h, i, n * B, B, cos, sin)  # [n*B, 3D], k normed + roped
         kv = torch.empty((n * B, 2 * D), dtype=BF16, device=self.device)
         N.copy_rows(qkv, 3 * D, kv, 2 * D, n * B, 2 * D, src_offset=D)
         kv_all = torch.empty((cp_size * n * B, 2 * D), dtype=BF16, device=self.device)

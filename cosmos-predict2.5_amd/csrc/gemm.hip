@@ -19,6 +19,8 @@
 //                                     the cross-attention q projection + its q_norm (:401-404, :411-419 without
 //                                     RoPE) with cp25_head_rmsnorm_rope's partial sums, butterfly and roundings
 //                                     (cp25_common.h hn_*): bit-identical to the GEMM followed by that kernel.
+//                     CP25_EPI_QKV  : the fused q|k|v projection with the k columns' RMSNorm + 3D RoPE in the
+//                                     epilogue (cp25_head_rmsnorm_rope's arithmetic again), q and v as bf16(acc).
 //
 // Design (MI355X, see DESIGN.md §3 "GEMM"): 256 x 256 output tile per 512-thread workgroup (one per
 // CU), 8 waves as 2 (M) x 4 (N), each wave 128 x 64 with v_mfma_f32_16x16x32_bf16 (32 accumulators,
@@ -51,6 +53,15 @@ constexpr int kGroupM = 8;
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 
+// compile-time loop: f(integral_constant<int, I>) for I = 0 .. N-1, in order
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
+}
+
 // one 16-B-per-lane buffer_load ... lds piece (a plain __device__ function: inside the kernel template the host pass
 // drops the kernel's launch stub over this builtin)
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, lds_void_ptr dst, int voffset, int soffset) {
@@ -68,6 +79,9 @@ struct ResEpi {
   const unsigned short* gate; int64_t g_sb, g_st;
   int B; int64_t tok0, hw;
   const unsigned short* nw; float n_eps, n_scale;
+  // CP25_EPI_QKV: output columns [n_lo, n_hi) (the k projection) get nw's per-head RMSNorm and the rotate-half RoPE of
+  // token row / B (rcos / rsin [tokens][64] fp32; nullptr: none), the others pass through
+  const float* rcos; const float* rsin; int n_lo, n_hi;
 };
 
 // x + gate * y on 8 bf16 columns, two bf16 roundings (the reference's two torch ops, = cp25_ln_mod's residual)
@@ -419,7 +433,7 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
   int tile = my_slot;
   if (tile >= n_tiles) return;
   u32x4 nwv = {0u, 0u, 0u, 0u};  // CP25_EPI_HNORM: this lane's 8 norm weights (columns 8 (ch & 15) .. of its head)
-  if constexpr (kEpi == CP25_EPI_HNORM) nwv = *reinterpret_cast<const u32x4*>(re.nw + (tid & 15) * 8);
+  if constexpr (kEpi == CP25_EPI_HNORM || kEpi == CP25_EPI_QKV) nwv = *reinterpret_cast<const u32x4*>(re.nw + (tid & 15) * 8);
   if constexpr (kEpi == CP25_EPI_GELU) {  // the GELU table (visible after the prologue's barrier)
     unsigned short* tab = reinterpret_cast<unsigned short*>(smem + 2 * kBuf8);
     for (int i = tid; i < kGeluTab; i += kThreads) {
@@ -557,6 +571,71 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
     for (int it = 0; it < 16; ++it) cv[it] = *reinterpret_cast<const u32x4*>(rd + it * 16 * 256);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // the LDS is free for the next tile's DMA
+    if constexpr (kEpi == CP25_EPI_QKV) {
+      if (n0 >= re.n_lo && n0 < re.n_hi) {  // a k tile (wave-uniform): RMSNorm + RoPE of its two heads per row
+        // the tile's RoPE rows (tokens m0 / B .., 256 / B of them) come into the free LDS first (by LDS-DMA, one
+        // exposed round trip; loaded per row into registers they were 16 serialised trips: +0.8 ms per launch)
+        const int li = ch & 15, dlo = (li & 7) * 8;
+        const float sgn = li < 8 ? -1.f : 1.f;
+        const bool rope = re.rcos != nullptr;
+        const int tok_lo = m0 / re.B;
+        constexpr int kTabBytes = 65536;  // per table: up to 256 tokens x 64 fp32
+        if (rope) {
+          const int ntok = min(M - 1, m0 + kBM - 1) / re.B - tok_lo + 1;
+          const int nbytes = ntok * 256;
+          const __amdgpu_buffer_rsrc_t c_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+              (void*)(re.rcos + (int64_t)tok_lo * 64), (short)0, nbytes, 0x00020000);
+          const __amdgpu_buffer_rsrc_t s_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+              (void*)(re.rsin + (int64_t)tok_lo * 64), (short)0, nbytes, 0x00020000);
+          for (int kb = wave; kb * 1024 < nbytes; kb += kThreads / 64) {  // 1 KiB (4 tokens) per wave instruction
+            dma16(c_rsrc, (lds_void_ptr)(smem + kb * 1024), kb * 1024 + 16 * lane, 0);
+            dma16(s_rsrc, (lds_void_ptr)(smem + kTabBytes + kb * 1024), kb * 1024 + 16 * lane, 0);
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+        }
+        const float* const tcos = reinterpret_cast<const float*>(smem);
+        const float* const tsin = reinterpret_cast<const float*>(smem + kTabBytes);
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+          float v[8];
+#pragma unroll
+          for (int w2 = 0; w2 < 4; ++w2) {
+            v[2 * w2] = bf2f((unsigned short)(cv[it][w2] & 0xffffu));
+            v[2 * w2 + 1] = bf2f((unsigned short)(cv[it][w2] >> 16));
+          }
+          float ss = hn_sumsq8(v);
+#pragma unroll
+          for (int m = 8; m >= 1; m >>= 1) ss += __shfl_xor(ss, m, 16);
+          const float rstd = hn_rstd(ss, re.n_eps);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            v[e] = hn_norm(v[e], rstd, bf2f((unsigned short)(nwv[e >> 1] >> (16 * (e & 1)))));
+          if (rope) {
+            const int tl = min(m0 + r0 + 16 * it, M - 1) / re.B - tok_lo;
+            const f32x4 c0 = *reinterpret_cast<const f32x4*>(tcos + tl * 64 + dlo);
+            const f32x4 c1 = *reinterpret_cast<const f32x4*>(tcos + tl * 64 + dlo + 4);
+            const f32x4 s0 = *reinterpret_cast<const f32x4*>(tsin + tl * 64 + dlo);
+            const f32x4 s1 = *reinterpret_cast<const f32x4*>(tsin + tl * 64 + dlo + 4);
+            float partner[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) partner[e] = __shfl_xor(v[e], 8, 16);
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              v[e] = hn_rope(v[e], partner[e], sgn, e < 4 ? c0[e & 3] : c1[e & 3], e < 4 ? s0[e & 3] : s1[e & 3]);
+          }
+          u32x4 o;
+#pragma unroll
+          for (int w2 = 0; w2 < 4; ++w2)
+            o[w2] = (unsigned)f2bf(v[2 * w2] * re.n_scale) | ((unsigned)f2bf(v[2 * w2 + 1] * re.n_scale) << 16);
+          cv[it] = o;
+        }
+        if (rope) {  // every wave's table reads are done before the next tile's DMA writes the LDS
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+        }
+      }
+    }
     if constexpr (kEpi == CP25_EPI_RES) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the x / gate chunks (nothing else is in flight)
 #pragma unroll
@@ -627,9 +706,15 @@ static int gemm_launch(const void* a, int64_t lda, const void* w, int64_t ldw, v
   if (lda < K || ldw < K || ldc < N || (lda % 8) || (ldw % 8) || (ldc % 8)) return CP25_ERR_INVAL;
   if (lda >= (1 << 22) || ldw >= (1 << 22)) return CP25_ERR_INVAL;  // 32-bit in-tile byte offsets
   if (((uintptr_t)a | (uintptr_t)w | (uintptr_t)c) & 15) return CP25_ERR_INVAL;
-  if (epilogue != CP25_EPI_NONE && epilogue != CP25_EPI_GELU && epilogue != CP25_EPI_RES && epilogue != CP25_EPI_HNORM)
+  if (epilogue != CP25_EPI_NONE && epilogue != CP25_EPI_GELU && epilogue != CP25_EPI_RES && epilogue != CP25_EPI_HNORM &&
+      epilogue != CP25_EPI_QKV)
     return CP25_ERR_INVAL;
-  if (epilogue == CP25_EPI_HNORM) {
+  if (epilogue == CP25_EPI_QKV) {
+    if (re.B <= 0 || re.n_lo < 0 || re.n_hi > N || re.n_lo % kBN || re.n_hi % kBN || re.n_lo >= re.n_hi ||
+        (!re.rcos) != (!re.rsin) || (((uintptr_t)re.rcos | (uintptr_t)re.rsin) & 15))
+      return CP25_ERR_INVAL;
+  }
+  if (epilogue == CP25_EPI_HNORM || epilogue == CP25_EPI_QKV) {
     if (!re.nw || ((uintptr_t)re.nw & 15) || !(re.n_eps >= 0.f) || !(re.n_scale > 0.f)) return CP25_ERR_INVAL;
     if ((K / kBK) % 2 != 0) return CP25_ERR_DTYPE;  // the persistent kernel only (the caller runs the separate norm)
   }
@@ -675,6 +760,10 @@ static int gemm_launch(const void* a, int64_t lda, const void* w, int64_t ldw, v
         break;
       case CP25_EPI_HNORM:
         hipLaunchKernelGGL((gemm_nt_8ph<CP25_EPI_HNORM, 2>), pgrid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K,
+                           re, nullptr, nullptr);
+        break;
+      case CP25_EPI_QKV:
+        hipLaunchKernelGGL((gemm_nt_8ph<CP25_EPI_QKV, 2>), pgrid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K,
                            re, nullptr, nullptr);
         break;
       default:
@@ -745,9 +834,25 @@ extern "C" int cp25_gemm_hnorm(const void* a, int64_t lda, const void* w, int64_
   return gemm_launch(a, lda, w, ldw, c, ldc, M, N, K, CP25_EPI_HNORM, re, stream);
 }
 
+extern "C" int cp25_gemm_qkv(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int M,
+                             int N, int K, int k_col0, int k_cols, const void* k_norm_weight, const float* cos_tab,
+                             const float* sin_tab, int B, float eps, hipStream_t stream) {
+  ResEpi re{};
+  re.nw = (const unsigned short*)k_norm_weight;
+  re.n_eps = eps;
+  re.n_scale = 1.f;
+  re.rcos = cos_tab;
+  re.rsin = sin_tab;
+  re.B = B;
+  re.n_lo = k_col0;
+  re.n_hi = k_col0 + k_cols;
+  return gemm_launch(a, lda, w, ldw, c, ldc, M, N, K, CP25_EPI_QKV, re, stream);
+}
+
 extern "C" int cp25_gemm_epi(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int M,
                              int N, int K, int epilogue, hipStream_t stream) {
-  if (epilogue == CP25_EPI_RES || epilogue == CP25_EPI_HNORM) return CP25_ERR_INVAL;  // their operands: _res / _hnorm
+  if (epilogue == CP25_EPI_RES || epilogue == CP25_EPI_HNORM || epilogue == CP25_EPI_QKV)
+    return CP25_ERR_INVAL;  // their operands: _res / _hnorm / _qkv
   const ResEpi re{};
   return gemm_launch(a, lda, w, ldw, c, ldc, M, N, K, epilogue, re, stream);
 }

@@ -247,6 +247,7 @@ int cp25_gelu(void* x, int64_t n, hipStream_t stream);
 #define CP25_EPI_GELU 1
 #define CP25_EPI_RES 2
 #define CP25_EPI_HNORM 3
+#define CP25_EPI_QKV 4
 int cp25_gemm_epi(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int M, int N, int K,
                   int epilogue, hipStream_t stream);
 
@@ -258,6 +259,16 @@ int cp25_gemm_epi(const void* a, int64_t lda, const void* w, int64_t ldw, void* 
  * CP25_ERR_DTYPE: run the two ops). */
 int cp25_gemm_hnorm(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int M, int N, int K,
                     const void* norm_weight, float eps, float out_scale, hipStream_t stream);
+
+/* The fused q|k|v projection with the k columns' per-head RMSNorm + 3D RoPE in the epilogue (CP25_EPI_QKV): output
+ * columns [k_col0, k_col0 + k_cols) (multiples of 256) get cp25_head_rmsnorm_rope's arithmetic with k_norm_weight
+ * [128] bf16, eps and the rotate-half RoPE of token row / B (cos_tab / sin_tab [M / B][64] fp32; both NULL: none),
+ * the other columns are bf16(A W^T): bit-identical to cp25_gemm_epi followed by cp25_head_rmsnorm_rope on the k
+ * columns, one HBM pass over k fewer (Attention.compute_qkv's k_proj + k_norm + RoPE, minimal_v4_dit.py:401-419).
+ * K / 64 must be even (else CP25_ERR_DTYPE: run the two ops). */
+int cp25_gemm_qkv(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int M, int N, int K,
+                  int k_col0, int k_cols, const void* k_norm_weight, const float* cos_tab, const float* sin_tab, int B,
+                  float eps, hipStream_t stream);
 
 /* cp25_gemm_epi with the block's gated residual as the epilogue: C = bf16(x + bf16(gate * bf16(A W^T))), the two
  * bf16 roundings of the reference's `x + gate * y` (cp25_ln_mod's residual, bit for bit). Output row r is token

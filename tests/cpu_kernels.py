@@ -167,6 +167,16 @@ def gemm_hnorm(a, w, norm_weight, *, out_scale=1.0, eps=1e-6, out=None):
     return out
 
 
+def gemm_qkv(a, w, k_norm_weight, *, k_col0, k_cols, B, cos=None, sin=None, eps=1e-6, out=None):
+    y = F.linear(a, w)
+    head_rmsnorm_rope(y, n_rows=y.shape[0], B=B, H=k_cols // 128, head_off=k_col0, weight=k_norm_weight, cos=cos,
+                      sin=sin, eps=eps)
+    if out is None:
+        return y
+    out.copy_(y)
+    return out
+
+
 def vae_attn(q, k, v, out=None, scale=None):
     sc = q.shape[-1] ** -0.5 if scale is None else scale
     p = torch.softmax(torch.einsum("tld,tmd->tlm", q.double(), k.double()) * sc, -1)
@@ -179,7 +189,7 @@ def vae_attn(q, k, v, out=None, scale=None):
 
 _FUNCS = dict(conv3d=conv3d, rms_norm_silu=rms_norm_silu, vae_attn=vae_attn, ln_mod=ln_mod, final_ln_mod=final_ln_mod, head_rmsnorm_rope=head_rmsnorm_rope, copy_rows=copy_rows,
               attn_fwd=attn_fwd, attn_kernel_name=attn_kernel_name, gemm_epi=gemm_epi, gemm_res=gemm_res,
-              gemm_hnorm=gemm_hnorm, gelu_=gelu_)
+              gemm_hnorm=gemm_hnorm, gemm_qkv=gemm_qkv, gelu_=gelu_)
 
 
 @contextlib.contextmanager

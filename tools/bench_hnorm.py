@@ -1,6 +1,7 @@
-"""The cross-attention q projection at the metric shape (M = 218 240, 2048 x 2048): own GEMM + the separate q
-RMSNorm pass (cp25_gemm_epi + cp25_head_rmsnorm_rope_scaled) vs the fused epilogue (cp25_gemm_hnorm), HIP events,
-interleaved rounds in one process. One JSON line.
+"""The projections whose head norm moved into the GEMM epilogue, at the metric shape (M = 218 240): the cross-attention
+q (2048 x 2048; cp25_gemm_epi + cp25_head_rmsnorm_rope_scaled vs cp25_gemm_hnorm) and the fused QKV (6144 x 2048;
+cp25_gemm_epi + the k RMSNorm + RoPE pass vs cp25_gemm_qkv), HIP events, interleaved rounds in one process. One JSON
+line per projection.
 usage: python tools/bench_hnorm.py [--rounds 3]"""
 import argparse
 import json
@@ -52,7 +53,27 @@ def main():
         res["two_pass_ms"].append(timed(two_pass))
         res["fused_ms"].append(timed(fused))
         res["gemm_only_ms"].append(timed(lambda: N.gemm_epi(x, w, out=out)))
-    print(json.dumps({"shape": f"M={M} N={D} K={D}", **res, "min_two_pass": min(res["two_pass_ms"]),
+    print(json.dumps({"proj": "cross-q", "shape": f"M={M} N={D} K={D}", **res, "min_two_pass": min(res["two_pass_ms"]),
+                      "min_fused": min(res["fused_ms"]), "min_gemm_only": min(res["gemm_only_ms"])}), flush=True)
+    # the QKV projection: k columns normed + RoPE (B = 2 token-major rows)
+    w3 = (torch.randn(3 * D, D, device=dev, generator=g) * D ** -0.5).to(torch.bfloat16)
+    out3 = torch.empty(M, 3 * D, device=dev, dtype=torch.bfloat16)
+    ang = torch.rand(M // 2, 64, device=dev, generator=g) * 50.0
+    cos, sin = torch.cos(ang).contiguous(), torch.sin(ang).contiguous()
+
+    def two_pass3():
+        N.gemm_epi(x, w3, out=out3)
+        N.head_rmsnorm_rope(out3, n_rows=M, B=2, H=D // 128, head_off=D, weight=nw, cos=cos, sin=sin)
+
+    def fused3():
+        N.gemm_qkv(x, w3, nw, k_col0=D, k_cols=D, B=2, cos=cos, sin=sin, out=out3)
+
+    res = {"two_pass_ms": [], "fused_ms": [], "gemm_only_ms": []}
+    for _ in range(a.rounds):
+        res["two_pass_ms"].append(timed(two_pass3))
+        res["fused_ms"].append(timed(fused3))
+        res["gemm_only_ms"].append(timed(lambda: N.gemm_epi(x, w3, out=out3)))
+    print(json.dumps({"proj": "qkv", "shape": f"M={M} N={3 * D} K={D}", **res, "min_two_pass": min(res["two_pass_ms"]),
                       "min_fused": min(res["fused_ms"]), "min_gemm_only": min(res["gemm_only_ms"])}), flush=True)
 
 
