@@ -89,6 +89,7 @@ SIGNATURES = {
     "cp25_quant_fp8_rows": [_P, _P, _P, _I64, _I64, _P],
     "cp25_gelu_quant_fp8": [_P, _P, _P, _I64, _I64, _P],
     "cp25_patchify": [_P, _P, _P, _P, _P, _I64, _I64, _I64, _P],
+    "cp25_patchify_ld": [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _P],
     "cp25_cfg_velocity": [_P, _I, _P, _P, _P, _F, _I, _P, _I64, _I64, _I64, _P],
     "cp25_unipc_step": [_P, _P, _P, _P, _P, _I64, ctypes.POINTER(UniPCParams), _P],
     "cp25_conv3d": [ctypes.POINTER(ctypes.c_void_p), _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I,
@@ -639,15 +640,22 @@ def quant_fp8_rows(x: torch.Tensor, gelu: bool = False) -> Tuple[torch.Tensor, t
 
 
 def patchify(xs: torch.Tensor, gt: Optional[torch.Tensor], frame_mask: torch.Tensor,
-             pad_mask: Optional[torch.Tensor], *, tok0: int, hw: int) -> torch.Tensor:
+             pad_mask: Optional[torch.Tensor], *, tok0: int, hw: int, ld: int = 72) -> torch.Tensor:
+    """x_embedder input rows [n_tok, 72] bf16 (cp25_patchify). ld = 128: the rows live in a zero-padded
+    [n_tok, 128] buffer (cp25_patchify_ld) and the returned [n_tok, 72] view has row stride 128, the own GEMM's
+    K = 128 operand (DiT.embed_patches)."""
     lib = load_library()
     n_tok = xs.shape[0]
     _check_mask(frame_mask, n_tok=n_tok, tok0=tok0, hw=hw)
-    out = torch.empty((n_tok, 72), dtype=torch.bfloat16, device=xs.device)
-    rc = lib.cp25_patchify(_ptr(xs), _ptr(gt), _ptr(frame_mask), _ptr(pad_mask), _ptr(out), n_tok, tok0, hw,
-                           _stream(xs.device))
+    out = torch.empty((n_tok, ld), dtype=torch.bfloat16, device=xs.device)
+    if ld == 72:
+        rc = lib.cp25_patchify(_ptr(xs), _ptr(gt), _ptr(frame_mask), _ptr(pad_mask), _ptr(out), n_tok, tok0, hw,
+                               _stream(xs.device))
+    else:
+        rc = lib.cp25_patchify_ld(_ptr(xs), _ptr(gt), _ptr(frame_mask), _ptr(pad_mask), _ptr(out), int(ld), n_tok,
+                                  tok0, hw, _stream(xs.device))
     _check("cp25_patchify", rc)
-    return out
+    return out[:, :72]
 
 
 def cfg_velocity(net: torch.Tensor, noise: Optional[torch.Tensor], gt: Optional[torch.Tensor],

@@ -231,6 +231,7 @@ class MinimalV1LVGDiT:
         # the self-attention normalises its own q (cp25_attn_fwd_prescaled_qnorm: head_rmsnorm_rope's arithmetic on
         # the Q fragments as they load, bit-identical, no separate pass over q in HBM); prescaled bf16 form only
         self.fused_q_norm = True
+        self._x_embed_w128 = None  # the x_embedder weight zero-padded to K = 128 (embed_patches' own-GEMM path)
 
     def set_linear_precision(self, precision: str) -> None:
         """"bf16" (default, the reference's arithmetic) or "fp8": the 28 blocks' q/k/v, output, cross-q,
@@ -424,6 +425,7 @@ class MinimalV1LVGDiT:
         cfg = self.cfg
         dev = self.device
         self.sd = {k: v.to(device=dev, dtype=shapes[k][1]).contiguous() for k, v in sd.items()}
+        self._x_embed_w128 = None
         self._fp8_w = {}
         D = cfg.model_channels
         p = self.sd
@@ -619,6 +621,17 @@ class MinimalV1LVGDiT:
         n, Bx, f = patch_rows.shape
         w = p["x_embedder.proj.1.weight"]
         if not cfg.view_condition_dim:
+            if (Bx == 1 and f == 72 and patch_rows.stride(0) == 128 and patch_rows.stride(2) == 1 and
+                    self.block_gemm == "own" and N.gemm_supported(D, 128)):
+                # rows from patchify(ld=128): the zero-padded K = 128 operand of the own GEMM against the weight
+                # zero-padded to 128 columns (the same sums as K = 72; the library GEMM took K = 72 before)
+                a = torch.as_strided(patch_rows, (n, 128), (128, 1))
+                wp = self._x_embed_w128
+                if wp is None or wp.shape[0] != D:
+                    wp = torch.zeros((D, 128), dtype=BF16, device=self.device)
+                    wp[:, :f] = w[:, :f]
+                    self._x_embed_w128 = wp
+                return N.gemm_epi(a, wp).view(n, 1, D)
             return F.linear(patch_rows.reshape(n * Bx, f), w).view(n, Bx, D)
         V = geo.n_views
         if view_indices is None:

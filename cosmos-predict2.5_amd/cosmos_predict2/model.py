@@ -282,7 +282,7 @@ class SamplingRun:
             raise RuntimeError("the trajectory is complete (restart() to run it again)")
         m, geo = self.model, self.geo
         t = self.timesteps[self.i]
-        rows = N.patchify(self.x, self.gtp, self.frame_mask, None, tok0=geo.tok0, hw=geo.hw)
+        rows = N.patchify(self.x, self.gtp, self.frame_mask, None, tok0=geo.tok0, hw=geo.hw, ld=128)
         tf = m._frame_timesteps(t, self.frame_mask)  # [T]
         t_B_T = (tf[None, :] * m.net_cfg.timestep_scale).expand(2, geo.T).contiguous()
         if self.net_fn is None:

@@ -294,8 +294,8 @@ __global__ void __launch_bounds__(256) gelu_kernel(unsigned short* __restrict__ 
 __global__ void __launch_bounds__(256) patchify_kernel(const float* __restrict__ xs, const float* __restrict__ gt,
                                                        const float* __restrict__ frame_mask,
                                                        const unsigned short* __restrict__ pad_mask,
-                                                       unsigned short* __restrict__ out, int64_t n_tok,
-                                                       int64_t tok0, int64_t hw) {
+                                                       unsigned short* __restrict__ out, int64_t out_ld,
+                                                       int64_t n_tok, int64_t tok0, int64_t hw) {
   const int64_t tok = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int j = threadIdx.x & 63;  // j = p*16 + c
   if (tok >= n_tok) return;
@@ -310,12 +310,13 @@ __global__ void __launch_bounds__(256) patchify_kernel(const float* __restrict__
   } else {
     xin = x;
   }
-  unsigned short* o = out + tok * 72;
+  unsigned short* o = out + tok * out_ld;
   o[c * 4 + p] = f2bf(xin);
   if (j < 4) {
     o[64 + j] = f2bf(m);
     o[68 + j] = pad_mask != nullptr ? pad_mask[tok * 4 + j] : (unsigned short)0;
   }
+  for (int64_t z = 72 + j; z < out_ld; z += 64) o[z] = 0;  // a padded row (the own GEMM's K = 128): zero columns
 }
 
 // ---------------------------------------------------------------- GT velocity + CFG
@@ -489,7 +490,16 @@ extern "C" int cp25_patchify(const float* xs, const float* gt, const float* fram
                              int64_t n_tok, int64_t tok0, int64_t hw, hipStream_t stream) {
   if (!xs || !frame_mask || !out || n_tok <= 0 || hw <= 0) return CP25_ERR_INVAL;
   hipLaunchKernelGGL(patchify_kernel, dim3((unsigned)cdiv(n_tok, 4)), dim3(256), 0, stream, xs, gt, frame_mask,
-                     (const unsigned short*)pad_mask, (unsigned short*)out, n_tok, tok0, hw);
+                     (const unsigned short*)pad_mask, (unsigned short*)out, (int64_t)72, n_tok, tok0, hw);
+  CP25_LAUNCH_CHECK();
+  return CP25_OK;
+}
+
+extern "C" int cp25_patchify_ld(const float* xs, const float* gt, const float* frame_mask, const void* pad_mask,
+                                void* out, int64_t out_ld, int64_t n_tok, int64_t tok0, int64_t hw, hipStream_t stream) {
+  if (!xs || !frame_mask || !out || n_tok <= 0 || hw <= 0 || out_ld < 72 || out_ld % 8) return CP25_ERR_INVAL;
+  hipLaunchKernelGGL(patchify_kernel, dim3((unsigned)cdiv(n_tok, 4)), dim3(256), 0, stream, xs, gt, frame_mask,
+                     (const unsigned short*)pad_mask, (unsigned short*)out, out_ld, n_tok, tok0, hw);
   CP25_LAUNCH_CHECK();
   return CP25_OK;
 }

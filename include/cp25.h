@@ -306,6 +306,12 @@ int cp25_gemm_fp8_res(const void* a, int64_t lda, const float* a_scale, const vo
 int cp25_patchify(const float* xs, const float* gt, const float* frame_mask, const void* pad_mask, void* out,
                   int64_t n_tok, int64_t tok0, int64_t hw, hipStream_t stream);
 
+/* cp25_patchify into rows of out_ld elements (out_ld >= 72, a multiple of 8), columns 72 .. out_ld - 1 zeroed: with
+ * out_ld = 128 the rows are the K = 128 operand of the own GEMM (cp25_gemm_epi) against the x_embedder weight
+ * zero-padded to 128 columns, the same sums as K = 72. */
+int cp25_patchify_ld(const float* xs, const float* gt, const float* frame_mask, const void* pad_mask, void* out,
+                     int64_t out_ld, int64_t n_tok, int64_t tok0, int64_t hw, hipStream_t stream);
+
 /* v_out[tok, j] from the final-layer output net [n_tok, B, 64] fp32 (B = 1 or 2 = cond, uncond):
  * per branch v_b = (noise - gt) * mask + net_b * (1 - mask) (skipped if gt == NULL), then
  * cfg_mode 0: v = v_c + guidance (v_c - v_u)   (Video2World, video2world_model_rectified_flow.py:209)
