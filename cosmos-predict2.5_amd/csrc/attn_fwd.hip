@@ -229,6 +229,100 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
   const unsigned short* kp = a.k + b * a.k_sb + h * a.k_sh + (int64_t)key0 * a.k_sl;
   const unsigned short* vp = a.v + b * a.v_sb + h * a.v_sh + (int64_t)key0 * a.v_sl;
 
+  const int ntiles = kPersist ? (blk_end - blk0) * ntk : ntk;
+  const int copy_tile = kPersist && ntk > 1 ? (kQCopyStagger ? (int)(blockIdx.x % (unsigned)(ntk - 1)) : 0) : 0;
+
+  // staging: a group's 256 threads own rows u/16 + 16 i, chunk u%16 of a 64 x 128 tile. buffer_load with a
+  // wave-uniform descriptor (SALU-only addressing); rows past Lk fall outside its range and read as zero (their
+  // scores are masked to -inf)
+  const int u = tid & (kThreads / 2 - 1);
+  const int srow = u >> 4, sch = u & 15;
+  const int64_t sl = group_b ? a.k_sl : a.v_sl;
+  const char* sbase = group_b ? (const char*)kp : (const char*)vp;
+  const int st_off = (int)(srow * sl * 2) + sch * 16, st_step = (int)(16 * sl * 2);
+  u32x4 st[4];
+  auto load_tile = [&](int t) __attribute__((always_inline)) {
+    const char* base;
+    int kt;
+    if constexpr (kPersist) {  // key tile kt of block blk0 + t / ntk (wave-uniform scalar arithmetic)
+      const int tb = t / ntk;
+      kt = t - tb * ntk;
+      const int bh_t = (blk0 + tb) / a.nqb;
+      const int b_t = bh_t / a.H, h_t = bh_t % a.H;
+      base = group_b ? (const char*)(a.k + b_t * a.k_sb + h_t * a.k_sh) : (const char*)(a.v + b_t * a.v_sb + h_t * a.v_sh);
+    } else {
+      kt = t;
+      base = sbase;
+    }
+    const int rows = (kPersist && t >= ntiles) ? 0 : min(Lk - kt * kKBlk, kKBlk);  // past the run: no bytes
+    const int nbytes = rows > 0 ? (int)((rows - 1) * sl * 2) + 2 * kD : 0;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(base + (int64_t)kt * kKBlk * sl * 2), (short)0, nbytes,
+                                                        0x00020000);
+    int off = st_off;
+    if constexpr (kPersist) {  // u = 64 (wave & 3) + lane: row u / 16, 16-B chunk u % 16
+      const int uf = ((wave_u & 3) << 6) + lane_fresh();
+      off = (uf >> 4) * (int)(sl * 2) + (uf & 15) * 16;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      st[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + i * st_step, 0, 0));
+  };
+  char* const k_wr = smem + srow * kKStride16 + sch * 16;
+  char* const v_wr = smem + VB0 + srow * kVStride16 + sch * 16;
+
+  // LDS-DMA staging (per-block kernels): K tiles always (group B), V tiles too in the online form (group A), straight
+  // into the padded 288-B rows, so the readers keep their immediate offsets and no staging VGPRs are live. The register
+  // path cost 4.7 % of the launch in load issue and register-file return (profiles/r3/attn_nop/staging_load_probe.log);
+  // by DMA: zero shift -1.95 %, online max -3.2 % (K and V; K alone spills in the online form, V by DMA in the zero-
+  // shift form measured slower), profiles/r3/attn_nop/dma_staging_ab.log. Instruction j of a group's wave wb moves tile
+  // bytes [1024 (wb + 4 j), +1024) of the 64 x 288-B image (18 per tile: waves 0-1 issue 5, waves 2-3 issue 4); lane l
+  // the 16 B at byte 16 l of it: row bb / 288, column bb % 288 (columns >= 256 are the row padding and re-read the
+  // tile's first 16 B). Rows past Lk on the ragged tile re-read row rows - 1: finite, and their scores are masked to
+  // -inf (K) or multiplied by P = 0 (V). The persistent form keeps the register path (its Q copy owns the DMA waits).
+  constexpr bool kDmaK = !kPersist;
+  constexpr bool kDmaV = kDmaK && online;
+  const int wb = wave_u & 3;  // wave within its group
+  int dma_off[5];             // lane source offsets of a full tile, per instruction
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int bb = 1024 * (wb + 4 * j) + 16 * lane;
+    const int row = bb / kKStride16, cb = bb - row * kKStride16;
+    dma_off[j] = cb < 2 * kD ? row * (int)(sl * 2) + cb : 0;
+  }
+  auto dma_tile = [&](int t, auto BUF) __attribute__((always_inline)) {  // group B: K(t), group A: V(t)
+    constexpr int kb = decltype(BUF)::value ? KB1 : 0;
+    const char* tsrc = sbase + (int64_t)t * kKBlk * sl * 2;
+    const int rows = min(Lk - t * kKBlk, kKBlk);
+    if (rows <= 0) return;  // no such tile (wave-uniform; callers stage only existing tiles)
+    const unsigned lds0 = (unsigned)(uintptr_t)(lds_char_ptr)(smem + (group_b ? kb : VB0 + (kb ? kVBuf16 : 0)));
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      if (wb + 4 * j >= 18) break;  // wave-uniform
+      int off = dma_off[j];
+      if (__builtin_expect(rows < kKBlk, 0)) {
+        const int bb = 1024 * (wb + 4 * j) + 16 * lane;
+        const int row = bb / kKStride16, cb = bb - row * kKStride16;
+        off = cb < 2 * kD ? min(row, rows - 1) * (int)(sl * 2) + cb : 0;
+      }
+      // inline asm (as dma_q): a compiler-visible LDS-DMA makes the compiler drain vmcnt before every s_barrier.
+      // M0 is reserved (never allocated); the s_nop 0 separates its write from the DMA that reads it.
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(tsrc),
+                   "s"(lds0 + 1024 * (wb + 4 * j)) : "memory");
+    }
+  };
+
+  // The first K / V tiles' LDS-DMA is issued here, before the Q loads: their latency overlaps the Q load's and the
+  // in-kernel q normalisation's (issued after them, the normalisation's VALU and the DMA round trip ran back to
+  // back in every workgroup's prologue). The prologue's vmcnt(0) below retires them.
+  if constexpr (kDmaK) {
+    if (group_b) {
+      dma_tile(0, std::integral_constant<int, 0>{});
+      if (ntiles > 1) dma_tile(1, std::integral_constant<int, 1>{});  // only tiles that exist (unsigned row clamp)
+    } else if constexpr (kDmaV) {
+      dma_tile(0, std::integral_constant<int, 0>{});  // V(0)
+    }
+  }
+
   // ---- Q fragments (B operand): Q[16 qh + c][32 s + 8 g .. +7] ----
   int q_row[2];
   bf16x8 qf[2][4];
@@ -331,7 +425,10 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
     for (int w = 0; w < kWaves; ++w) qm = fmaxf(qm, gate_max[w]);
     // bound product with a 1e-3 margin (fp32 sums of the scores and of the norms); no slots written: online
     const bool zero_ok = km > 0.f && qm * km * 1.001f <= kTop;
-    if (zero_ok != (kGate == 1)) return;  // uniform over the workgroup
+    if (zero_ok != (kGate == 1)) {  // uniform over the workgroup
+      if constexpr (kDmaK) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup
+      return;
+    }
   }
 
   f32x4 o[8][2];
@@ -364,87 +461,6 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
 #pragma unroll
   for (int qh = 0; qh < 2; ++qh) minit[qh] = f32x4{-m_run[qh], -m_run[qh], -m_run[qh], -m_run[qh]};
 
-  const int ntiles = kPersist ? (blk_end - blk0) * ntk : ntk;
-  const int copy_tile = kPersist && ntk > 1 ? (kQCopyStagger ? (int)(blockIdx.x % (unsigned)(ntk - 1)) : 0) : 0;
-
-  // staging: a group's 256 threads own rows u/16 + 16 i, chunk u%16 of a 64 x 128 tile. buffer_load with a
-  // wave-uniform descriptor (SALU-only addressing); rows past Lk fall outside its range and read as zero (their
-  // scores are masked to -inf)
-  const int u = tid & (kThreads / 2 - 1);
-  const int srow = u >> 4, sch = u & 15;
-  const int64_t sl = group_b ? a.k_sl : a.v_sl;
-  const char* sbase = group_b ? (const char*)kp : (const char*)vp;
-  const int st_off = (int)(srow * sl * 2) + sch * 16, st_step = (int)(16 * sl * 2);
-  u32x4 st[4];
-  auto load_tile = [&](int t) __attribute__((always_inline)) {
-    const char* base;
-    int kt;
-    if constexpr (kPersist) {  // key tile kt of block blk0 + t / ntk (wave-uniform scalar arithmetic)
-      const int tb = t / ntk;
-      kt = t - tb * ntk;
-      const int bh_t = (blk0 + tb) / a.nqb;
-      const int b_t = bh_t / a.H, h_t = bh_t % a.H;
-      base = group_b ? (const char*)(a.k + b_t * a.k_sb + h_t * a.k_sh) : (const char*)(a.v + b_t * a.v_sb + h_t * a.v_sh);
-    } else {
-      kt = t;
-      base = sbase;
-    }
-    const int rows = (kPersist && t >= ntiles) ? 0 : min(Lk - kt * kKBlk, kKBlk);  // past the run: no bytes
-    const int nbytes = rows > 0 ? (int)((rows - 1) * sl * 2) + 2 * kD : 0;
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(base + (int64_t)kt * kKBlk * sl * 2), (short)0, nbytes,
-                                                        0x00020000);
-    int off = st_off;
-    if constexpr (kPersist) {  // u = 64 (wave & 3) + lane: row u / 16, 16-B chunk u % 16
-      const int uf = ((wave_u & 3) << 6) + lane_fresh();
-      off = (uf >> 4) * (int)(sl * 2) + (uf & 15) * 16;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      st[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + i * st_step, 0, 0));
-  };
-  char* const k_wr = smem + srow * kKStride16 + sch * 16;
-  char* const v_wr = smem + VB0 + srow * kVStride16 + sch * 16;
-
-  // LDS-DMA staging (per-block kernels): K tiles always (group B), V tiles too in the online form (group A), straight
-  // into the padded 288-B rows, so the readers keep their immediate offsets and no staging VGPRs are live. The register
-  // path cost 4.7 % of the launch in load issue and register-file return (profiles/r3/attn_nop/staging_load_probe.log);
-  // by DMA: zero shift -1.95 %, online max -3.2 % (K and V; K alone spills in the online form, V by DMA in the zero-
-  // shift form measured slower), profiles/r3/attn_nop/dma_staging_ab.log. Instruction j of a group's wave wb moves tile
-  // bytes [1024 (wb + 4 j), +1024) of the 64 x 288-B image (18 per tile: waves 0-1 issue 5, waves 2-3 issue 4); lane l
-  // the 16 B at byte 16 l of it: row bb / 288, column bb % 288 (columns >= 256 are the row padding and re-read the
-  // tile's first 16 B). Rows past Lk on the ragged tile re-read row rows - 1: finite, and their scores are masked to
-  // -inf (K) or multiplied by P = 0 (V). The persistent form keeps the register path (its Q copy owns the DMA waits).
-  constexpr bool kDmaK = !kPersist;
-  constexpr bool kDmaV = kDmaK && online;
-  const int wb = wave_u & 3;  // wave within its group
-  int dma_off[5];             // lane source offsets of a full tile, per instruction
-#pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    const int bb = 1024 * (wb + 4 * j) + 16 * lane;
-    const int row = bb / kKStride16, cb = bb - row * kKStride16;
-    dma_off[j] = cb < 2 * kD ? row * (int)(sl * 2) + cb : 0;
-  }
-  auto dma_tile = [&](int t, auto BUF) __attribute__((always_inline)) {  // group B: K(t), group A: V(t)
-    constexpr int kb = decltype(BUF)::value ? KB1 : 0;
-    const char* tsrc = sbase + (int64_t)t * kKBlk * sl * 2;
-    const int rows = min(Lk - t * kKBlk, kKBlk);
-    if (rows <= 0) return;  // no such tile (wave-uniform; callers stage only existing tiles)
-    const unsigned lds0 = (unsigned)(uintptr_t)(lds_char_ptr)(smem + (group_b ? kb : VB0 + (kb ? kVBuf16 : 0)));
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      if (wb + 4 * j >= 18) break;  // wave-uniform
-      int off = dma_off[j];
-      if (__builtin_expect(rows < kKBlk, 0)) {
-        const int bb = 1024 * (wb + 4 * j) + 16 * lane;
-        const int row = bb / kKStride16, cb = bb - row * kKStride16;
-        off = cb < 2 * kD ? min(row, rows - 1) * (int)(sl * 2) + cb : 0;
-      }
-      // inline asm (as dma_q): a compiler-visible LDS-DMA makes the compiler drain vmcnt before every s_barrier.
-      // M0 is reserved (never allocated); the s_nop 0 separates its write from the DMA that reads it.
-      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(tsrc),
-                   "s"(lds0 + 1024 * (wb + 4 * j)) : "memory");
-    }
-  };
   auto write_k = [&](auto BUF) __attribute__((always_inline)) {
     constexpr int kb = decltype(BUF)::value ? KB1 : 0;
 #pragma unroll
@@ -680,13 +696,9 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
 
   // ---- prologue: K(0), V(0) -> buffer 0; K(1) -> buffer 1; S(0) for everyone, P(0) for A ----
   if (kDmaK && group_b) {
-    // only tiles that exist: past the last one the row clamp would go negative (the DMA's VGPR offset is unsigned)
-    dma_tile(0, B0{});
-    if (ntiles > 1) dma_tile(1, B1{});
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K(0), K(1): issued before the Q loads
   } else if (kDmaV) {
-    dma_tile(0, B0{});  // V(0)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // V(0)
   } else {
     load_tile(0);
     if (group_b) write_k(B0{}); else write_v(B0{});
