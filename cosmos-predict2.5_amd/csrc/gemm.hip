@@ -290,12 +290,16 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
   const int wr = wave >> 2, wc = wave & 3;
   const int my_slot = xcd_remap(blockIdx.x, gridDim.x);
 
+  // L2 grouping: 8 row tiles per group; 16 for the bf16 8192-wide MLP layer1 (same box, plain GEMMs at M = 218 240,
+  // profiles/r4/gemm/group_ab.log: MLP1 5.48 vs 5.55 ms with 16, while QKV, MLP2 and the 2048-wide projections lose
+  // 1.3-2 % with it). Tile order only: results bit-identical.
+  const int gm = (kES == 2 && N >= 8192) ? 16 : kGroupM;
   auto tile_mn = [&](int tile, int& m0, int& n0) __attribute__((always_inline)) {
-    const int group = tile / (kGroupM * nt);
-    const int first_m = group * kGroupM;
-    const int gsize = min(mt - first_m, kGroupM);
-    m0 = (first_m + (tile % (kGroupM * nt)) % gsize) * kBM;
-    n0 = ((tile % (kGroupM * nt)) / gsize) * kBN;
+    const int group = tile / (gm * nt);
+    const int first_m = group * gm;
+    const int gsize = min(mt - first_m, gm);
+    m0 = (first_m + (tile % (gm * nt)) % gsize) * kBM;
+    n0 = ((tile % (gm * nt)) / gsize) * kBN;
   };
 
   // ---- DMA (buffer_load ... lds): wave w fills pieces 2w, 2w+1 (8 rows each) of every half-tile; lane l -> row

@@ -5,7 +5,8 @@ usage: python tools/lab/gemm_variant.py <name> <patch>[,<patch>...]  ->  tools/l
 patches: nostage (accumulators not written to the LDS C image), nostore (no global C stores), none;
 correct-result variants: sc1 (full-tile C stores write-through, dropping the lines from the XCD L2, via a buffer
 store with the sc1 policy bit), stagger<N> (workgroup w sleeps ((w >> 3) & 15) x s_sleep N before its first tile, so
-the workgroups' tile seams -- and their C-store bursts -- no longer coincide chip-wide)"""
+the workgroups' tile seams -- and their C-store bursts -- no longer coincide chip-wide), group<G> (kGroupM = G row
+tiles per L2 group instead of 8)"""
 import os
 import subprocess
 import sys
@@ -27,6 +28,8 @@ PATCHES = {
              "      for (int it = 0; it < 16; ++it) __builtin_amdgcn_raw_buffer_store_b128(cv[it], c_rsrc, c_off + it * 16 * (int)ldc * 2, 0, 16);\n")],
     "none": [],
 }
+for _g in (2, 4, 16, 32):  # the L2 grouping of row tiles (tile order only: bit-identical results)
+    PATCHES[f"group{_g}"] = [("constexpr int kGroupM = 8;\n", f"constexpr int kGroupM = {_g};\n")]
 for _n in (4, 8, 16, 32):
     PATCHES[f"stagger{_n}"] = [("  if (tile >= n_tiles) return;\n",
                                 "  if (tile >= n_tiles) return;\n"
