@@ -44,6 +44,27 @@ constexpr float kLazy = 24.f;       // online max: rescale only when a row max e
 
 typedef __attribute__((address_space(3))) const char* lds_char_ptr;
 
+// cp25_common.h's hn_* pieces on element pairs (v_pk_* f32): per element the same IEEE operations, contraction off
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 hn2_sumsq8(const f32x2* x) {  // two sequential 8-term chains
+#pragma clang fp contract(off)
+  f32x2 ss = {0.f, 0.f};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ss += x[e] * x[e];
+  return ss;
+}
+__device__ __forceinline__ f32x2 hn2_norm(f32x2 x, f32x2 rstd, f32x2 w) {
+#pragma clang fp contract(off)
+  const f32x2 t = (x * rstd) * w;
+  return __builtin_convertvector(__builtin_convertvector(t, bf16x2v), f32x2);  // rbf
+}
+__device__ __forceinline__ f32x2 hn2_rope(f32x2 v, f32x2 partner, float sgn, f32x2 c, f32x2 s) {
+#pragma clang fp contract(off)
+  const f32x2 sg = {sgn, sgn};
+  return __builtin_elementwise_fma(v, c, (sg * partner) * s);
+}
+
 // compile-time loop: f(integral_constant<int, I>) for I = 0 .. N-1, in order
 template <int N, int I = 0, class F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -358,41 +379,60 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
             }
         }
       }
+      // packed: element pairs (e, e + 1) through v_pk_* f32 (two of the scalar pieces' IEEE operations per instruction,
+      // the prologue runs on otherwise idle SIMDs); the sums of squares as two chains (s, s + 1) at once
+      const f32x2 scale2 = {a.qn_scale, a.qn_scale};
 #pragma unroll
       for (int qh = 0; qh < 2; ++qh) {
-        float x[4][8], p[4];
+        f32x2 x[4][4];  // [s][pair]: elements 2 pair, 2 pair + 1 of chunk s
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
+        for (int s = 0; s < 4; ++s)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) x[s][e] = static_cast<float>(qf[qh][s][e]);
-          p[s] = hn_sumsq8(x[s]);
+          for (int q = 0; q < 4; ++q)
+            x[s][q] = f32x2{static_cast<float>(qf[qh][s][2 * q]), static_cast<float>(qf[qh][s][2 * q + 1])};
+        f32x2 c01[8], c23[8];  // the chains of chunks (0, 1) and (2, 3), element by element
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          c01[e] = f32x2{x[0][e >> 1][e & 1], x[1][e >> 1][e & 1]};
+          c23[e] = f32x2{x[2][e >> 1][e & 1], x[3][e >> 1][e & 1]};
         }
-        const float a0 = p[0] + p[2], a1 = p[1] + p[3];
-        float ss = a0 + a1;
+        const f32x2 p01 = hn2_sumsq8(c01), p23 = hn2_sumsq8(c23);
+        const f32x2 aa = p01 + p23;  // {p0 + p2, p1 + p3}
+        float ss = aa.x + aa.y;
         ss += __shfl_xor(ss, 32);
         ss += __shfl_xor(ss, 16);
         const float rstd = hn_rstd(ss, a.qn_eps);
+        const f32x2 rstd2 = {rstd, rstd};
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) x[s][e] = hn_norm(x[s][e], rstd, static_cast<float>(wv[s][e]));
+          for (int q = 0; q < 4; ++q)
+            x[s][q] = hn2_norm(x[s][q], rstd2,
+                               f32x2{static_cast<float>(wv[s][2 * q]), static_cast<float>(wv[s][2 * q + 1])});
+        f32x2 y[4][4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) y[s][q] = x[s][q];
         if (rope) {
-          float y[4][8];
 #pragma unroll
           for (int s = 0; s < 4; ++s)
 #pragma unroll
-            for (int e = 0; e < 8; ++e)
-              y[s][e] = hn_rope(x[s][e], x[s ^ 2][e], s < 2 ? -1.f : 1.f, rc[qh][s & 1][e >> 2][e & 3],
-                                rsn[qh][s & 1][e >> 2][e & 3]);
-#pragma unroll
-          for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) x[s][e] = y[s][e];
+            for (int q = 0; q < 4; ++q) {
+              const f32x4 cc = rc[qh][s & 1][q >> 1], sn = rsn[qh][s & 1][q >> 1];
+              const int o = 2 * (q & 1);
+              y[s][q] = hn2_rope(x[s][q], x[s ^ 2][q], s < 2 ? -1.f : 1.f, f32x2{cc[o], cc[o + 1]},
+                                 f32x2{sn[o], sn[o + 1]});
+            }
         }
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) qf[qh][s][e] = static_cast<__bf16>(x[s][e] * a.qn_scale);
+          for (int q = 0; q < 4; ++q) {
+            const bf16x2v h = __builtin_convertvector(y[s][q] * scale2, bf16x2v);
+            qf[qh][s][2 * q] = h.x;
+            qf[qh][s][2 * q + 1] = h.y;
+          }
       }
     }
   }
