@@ -64,12 +64,13 @@ def _merge(a, b):
 def analyse(asm, name):
     """Per kernel: races found by a dataflow over the control-flow graph (each instruction's in-flight LDS reads are the
     join over its predecessors: fall-through, unless the previous instruction is an unconditional branch or the end of
-    the program, and every branch to its label), s_nop count, and in-loop scratch / vmcnt(0) counts."""
+    the program, and every branch to its label), s_nop counts (whole kernel and inside loops), and in-loop scratch /
+    vmcnt(0) counts."""
     i = asm.index(name + ":")
     j = asm.index(".Lfunc_end", i)
     lines = asm[i:j].split("\n")
     ins, labels, nops, m0nops = [], {}, 0, 0
-    inloop, scr, vm0 = False, 0, 0
+    inloop, scr, vm0, lnops = False, 0, 0, 0
     for l in lines:
         s = l.strip()
         if not s or s.startswith(";"):
@@ -92,6 +93,7 @@ def analyse(asm, name):
                 m0nops += 1  # the M0-write -> LDS-DMA separation the DMA asm carries, not a hazard pad
             else:
                 nops += 1
+                lnops += inloop
         ins.append((op, t, s))
     succ = []
     for k, (op, t, s) in enumerate(ins):
@@ -128,7 +130,8 @@ def analyse(asm, name):
             if state[q] is None or new != state[q]:
                 state[q] = new
                 work.append(q)
-    return {"races": [s for _, s in sorted(races)], "nops": nops, "m0_nops": m0nops, "inloop_scratch": scr, "inloop_vmcnt0": vm0}
+    return {"races": [s for _, s in sorted(races)], "nops": nops, "inloop_nops": lnops, "m0_nops": m0nops,
+            "inloop_scratch": scr, "inloop_vmcnt0": vm0}
 
 
 def check(src, flt=""):
