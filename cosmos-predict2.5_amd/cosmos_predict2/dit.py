@@ -226,7 +226,11 @@ class MinimalV1LVGDiT:
         # Off by default since round 4: with V staged by LDS-DMA the online-max form runs within 0.5 % of the zero-shift
         # loop (profiles/r4/attn_dma, r4ab_*), and without the gate a row's arithmetic never depends on its 256-row
         # block or on the other CFG entry's keys, so context-parallel shards stay bit-identical to CP = 1 with any
-        # checkpoint (tests/test_cp_gpu.py "nw_weight")
+        # checkpoint (tests/test_cp_gpu.py "nw_weight") -- under CP25_ATTN_SPLIT=1 only: by default the attention's
+        # tail split (cp25_attn_tail_workspace_bytes) runs the query blocks of a launch's last partial round as
+        # key-range splits, and which blocks those are depends on the launch's workgroup count mod the CU count, so
+        # it differs between CP = 1 and a shard (and between GPUs with different CU counts); those rows then differ
+        # from the unsplit ones by rounding (the same distance from fp32, tests/test_attn_m16_gpu.py)
         self.data_tight_k_bound = False
         # the self-attention normalises its own q (cp25_attn_fwd_prescaled_qnorm: head_rmsnorm_rope's arithmetic on
         # the Q fragments as they load, bit-identical, no separate pass over q in HBM); prescaled bf16 form only
@@ -609,8 +613,10 @@ class MinimalV1LVGDiT:
         return T // cfg.state_t
 
     def embed_patches(self, patch_rows: torch.Tensor, geo: Geometry,
-                      view_indices: Optional[torch.Tensor] = None) -> torch.Tensor:
+                      view_indices: Optional[torch.Tensor] = None, rows_k128: bool = False) -> torch.Tensor:
         """x_embedder (PatchEmbed Linear, minimal_v4_dit.py:846-913) of [n, Bx, 72] patch rows -> [n, Bx, D].
+        rows_k128: the caller made patch_rows with patchify(ld=128), i.e. they are the [:, :72] view of a [n, 128]
+        buffer whose columns 72.. the kernel zeroed; the own GEMM then multiplies the whole padded rows (K = 128)."""
         Multi-view nets also concatenate a view embedding as input channels
         (prepare_embedded_sequence, multiview_dit.py:462-490); those channels are constant over a view, so
         their patch features (c, p1, p2) fold into one per-view bias: y = rows W72^T + e_v Wv^T, summed
@@ -621,8 +627,9 @@ class MinimalV1LVGDiT:
         n, Bx, f = patch_rows.shape
         w = p["x_embedder.proj.1.weight"]
         if not cfg.view_condition_dim:
-            if (Bx == 1 and f == 72 and patch_rows.stride(0) == 128 and patch_rows.stride(2) == 1 and
-                    self.block_gemm == "own" and N.gemm_supported(D, 128)):
+            if rows_k128 and (Bx != 1 or f != 72 or patch_rows.stride(0) != 128 or patch_rows.stride(2) != 1):
+                raise ValueError("rows_k128: expected the [n, 1, 72] view of patchify(ld=128)'s [n, 128] buffer")
+            if rows_k128 and self.block_gemm == "own" and N.gemm_supported(D, 128):
                 # rows from patchify(ld=128): the zero-padded K = 128 operand of the own GEMM against the weight
                 # zero-padded to 128 columns (the same sums as K = 72; the library GEMM took K = 72 before)
                 a = torch.as_strided(patch_rows, (n, 128), (128, 1))
@@ -646,8 +653,10 @@ class MinimalV1LVGDiT:
 
     def forward_tokens(self, patch_rows: torch.Tensor, t_B_T: torch.Tensor, ctx: ContextCache,
                        geo: Geometry, action: Optional[torch.Tensor] = None,
-                       view_indices: Optional[torch.Tensor] = None, shared_batch: bool = False) -> torch.Tensor:
-        """patch_rows: [n_tok, Bx, 72] bf16 (Bx = 1 shares the input across the CFG batch);
+                       view_indices: Optional[torch.Tensor] = None, shared_batch: bool = False,
+                       rows_k128: bool = False) -> torch.Tensor:
+        """patch_rows: [n_tok, Bx, 72] bf16 (Bx = 1 shares the input across the CFG batch; rows_k128: made by
+        patchify(ld=128), see embed_patches);
         t_B_T: [B, T] fp32, already scaled. Returns the final layer output [n_tok, B, 64] fp32
         (feature order (p1 p2 C) = patch layout). shared_batch: the caller guarantees every batch entry
         has the same t (and action), so with Bx = 1 they differ only in the text context (_blocks).
@@ -665,7 +674,7 @@ class MinimalV1LVGDiT:
         D = cfg.model_channels
         n = geo.n_tok
         Bx = patch_rows.shape[1]
-        x_in = self.embed_patches(patch_rows, geo, view_indices)
+        x_in = self.embed_patches(patch_rows, geo, view_indices, rows_k128=rows_k128)
         mods, shift_f, scale_f = self.time_modulation(t_B_T, action)
         cos, sin = self.rope_tables(geo)
         cp = self.cp_group

@@ -289,7 +289,7 @@ class SamplingRun:
             # one t row expanded over the CFG pair, one action: the entries differ only in the text context
             shared = self.action is None or self.action.shape[0] == 1
             net_out = m.net.forward_tokens(rows.view(geo.n_tok, 1, -1), t_B_T, self.ctx, geo, action=self.action,
-                                           view_indices=self.view_indices, shared_batch=shared)
+                                           view_indices=self.view_indices, shared_batch=shared, rows_k128=True)
         else:
             net_out = self.net_fn(rows.view(geo.n_tok, 1, -1), t_B_T, geo)
         v = N.cfg_velocity(net_out, self.noise, self.gtp, self.frame_mask, self.guidance, self.mode,

@@ -125,6 +125,12 @@ struct AttnArgs {
   const float* qn_sin;
   float qn_eps, qn_scale;
   int qn_row0;
+#ifdef CP25_ATTN_PROBE
+  // lab build only (tools/attn_probe.py; the product build has no stamp): [probe_wg][8 waves][32 tiles][4] s_memtime
+  // stamps of workgroups blockIdx.x < probe_wg, tiles probe_t0 .. probe_t0 + 31
+  unsigned long long* probe;
+  int probe_t0, probe_wg;
+#endif
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -163,9 +169,12 @@ struct AttnArgs {
 // The host picks the mode from the bounds (m16_mode).
 constexpr int kKStride16 = 288;
 constexpr int kVStride16 = 288;
-// MFMA phase: operand pairs read ahead of their MFMAs. 2 (ring of 3 fragments) frees 4 VGPRs against 3: the online
-// form -3.4 % per launch, zero shift -0.1 %, 4: online +7 % (profiles/r3/attn_nop/ring_depth_ab.log, ring_depth2_ab.log)
-constexpr int kAhead = 2;
+// MFMA phase: operand pairs read ahead of their MFMAs (attn_fwd_m16's kAhead): 3 (a ring of 4 fragments) in the
+// per-block forms, 2 in the persistent cross-attention. Round 3 (register-path staging): 2 freed the 4 VGPRs the online
+// form spilled in its loop at 3 (-3.4 %), zero shift -0.1 %, 4: online +7 % (profiles/r3/attn_nop/ring_depth_ab.log,
+// ring_depth2_ab.log). Round 5: with K and V staged by LDS-DMA the loops hold 3 without spills: online -0.4..-0.9 %,
+// zero shift (with its V by DMA too) -0.25 % (profiles/r5/attn_iso/, profiles/r5/attn_ab/).
+constexpr int kAheadDefault = 2;
 constexpr int kKBuf16 = kKBlk * kKStride16;        // 18432
 constexpr int kVBuf16 = kKBlk * kVStride16;        // 18432
 constexpr int kLds16 = 2 * kKBuf16 + 2 * kVBuf16;  // 73728
@@ -219,6 +228,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
   static_assert(!kPersist || (kKind == 1 && kMode != 0), "persistent form: cross-attention, zero shift or online");
   constexpr bool online = kMode == 2;
   constexpr bool kInit = kPre && kMode != 1;  // the shift rides in the Q K^T chains' initial C
+  constexpr int kAhead = !kPersist ? 3 : kAheadDefault;  // MFMA-phase operand pairs read ahead
 
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   // persistent: this workgroup's run [blk0, blk_end) of blocks bh * nqb + qb (an XCD's workgroups hold one
@@ -245,6 +255,32 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
   const int g = lane >> 4;
   const bool group_b = __builtin_amdgcn_readfirstlane(tid) >= kThreads / 2;
   const int wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);  // the wave index as a scalar (persistent form)
+#ifdef CP25_ATTN_PROBE
+  // Lab probe (tools/attn_probe.py; per-block kernels only). Stamps go to the LDS (a global store would join the counted
+  // vmcnt waits) and are copied out at the end. Wait form (s_memtime + lgkmcnt(0)) only where the kernel leaves no LDS
+  // read in flight; group B's MFMA-phase start, where its pre-issued operand reads are in flight, takes the no-wait
+  // form (the counted lgkmcnt waits after it over-wait only while the s_memtime is outstanding) and is written after
+  // the phase's closing stamp.
+  __shared__ unsigned long long probe_lds[kWaves * 32 * 4];
+  unsigned long long probe_clk[4] = {0, 0, 0, 0};  // s_memtime, s_memrealtime (100 MHz) at the loop's start and end
+  const bool probe_on = !kPersist && kTail == 0 && a.probe != nullptr && (int)blockIdx.x < a.probe_wg;
+  int probe_t = -1;
+  unsigned long long probe_b2 = 0;
+#define ATTN_STAMP(T, K)                                                                                    \
+  do {                                                                                                      \
+    if (probe_on && (unsigned)((T) - a.probe_t0) < 32u) {                                                   \
+      __builtin_amdgcn_sched_barrier(0);                                                                    \
+      unsigned long long ts_;                                                                               \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts_)::"memory");                          \
+      probe_lds[(wave_u * 32 + (T) - a.probe_t0) * 4 + (K)] = ts_;                                         \
+      __builtin_amdgcn_sched_barrier(0);                                                                    \
+    }                                                                                                       \
+  } while (0)
+#else
+#define ATTN_STAMP(T, K) \
+  do {                   \
+  } while (0)
+#endif
 
   const unsigned short* qp = a.q + b * a.q_sb + h * a.q_sh;
   const unsigned short* kp = a.k + b * a.k_sb + h * a.k_sh + (int64_t)key0 * a.k_sl;
@@ -291,17 +327,18 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
   char* const k_wr = smem + srow * kKStride16 + sch * 16;
   char* const v_wr = smem + VB0 + srow * kVStride16 + sch * 16;
 
-  // LDS-DMA staging (per-block kernels): K tiles always (group B), V tiles too in the online form (group A), straight
-  // into the padded 288-B rows, so the readers keep their immediate offsets and no staging VGPRs are live. The register
-  // path cost 4.7 % of the launch in load issue and register-file return (profiles/r3/attn_nop/staging_load_probe.log);
-  // by DMA: zero shift -1.95 %, online max -3.2 % (K and V; K alone spills in the online form, V by DMA in the zero-
-  // shift form measured slower), profiles/r3/attn_nop/dma_staging_ab.log. Instruction j of a group's wave wb moves tile
+  // LDS-DMA staging (per-block kernels): K tiles (group B) and V tiles (group A) straight into the padded 288-B rows,
+  // so the readers keep their immediate offsets and no staging VGPRs are live. The register path cost 4.7 % of the
+  // launch in load issue and register-file return (profiles/r3/attn_nop/staging_load_probe.log); by DMA: zero shift
+  // -1.95 %, online max -3.2 % (profiles/r3/attn_nop/dma_staging_ab.log). Until round 4 the zero-shift form kept V on
+  // the register path (V by DMA measured 0.9 % slower there in round 3); round 5: V by DMA with the ring depth 3 it
+  // frees room for, -0.25 % (6 interleaved reps, profiles/r5/attn_ab/). Instruction j of a group's wave wb moves tile
   // bytes [1024 (wb + 4 j), +1024) of the 64 x 288-B image (18 per tile: waves 0-1 issue 5, waves 2-3 issue 4); lane l
   // the 16 B at byte 16 l of it: row bb / 288, column bb % 288 (columns >= 256 are the row padding and re-read the
   // tile's first 16 B). Rows past Lk on the ragged tile re-read row rows - 1: finite, and their scores are masked to
   // -inf (K) or multiplied by P = 0 (V). The persistent form keeps the register path (its Q copy owns the DMA waits).
   constexpr bool kDmaK = !kPersist;
-  constexpr bool kDmaV = kDmaK && online;
+  constexpr bool kDmaV = kDmaK;
   const int wb = wave_u & 3;  // wave within its group
   int dma_off[5];             // lane source offsets of a full tile, per instruction
 #pragma unroll
@@ -326,7 +363,9 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
         off = cb < 2 * kD ? min(row, rows - 1) * (int)(sl * 2) + cb : 0;
       }
       // inline asm (as dma_q): a compiler-visible LDS-DMA makes the compiler drain vmcnt before every s_barrier.
-      // M0 is reserved (never allocated); the s_nop 0 separates its write from the DMA that reads it.
+      // M0 is a reserved register the compiler never allocates (a clobber of it is ignored, with a warning); that no
+      // compiler-emitted instruction uses it in these kernels is checked in the ISA (tools/isa_check.py m0_uses).
+      // The s_nop 0 separates its write from the DMA that reads it.
       asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(tsrc),
                    "s"(lds0 + 1024 * (wb + 4 * j)) : "memory");
     }
@@ -755,6 +794,10 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
   if (!group_b) softmax(0);
   __syncthreads();
 
+#ifdef CP25_ATTN_PROBE
+  if (probe_on)
+    asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(probe_clk[0]), "=s"(probe_clk[1])::"memory");
+#endif
   // one MFMA phase: the 4 row-sum MFMAs, P.V of tile t, then Q K^T of tile t+1 (64 MFMAs of 16 cycles). Operand pair
   // n (one fragment, two MFMAs, one per query half): n < 16 the V^T fragment (db = n & 7, ks = n >> 3, two
   // transposed reads), n >= 16 the K fragment (kb = (n - 16) & 3, s = (n - 16) >> 2). (The Q K^T after the last tile
@@ -825,14 +868,26 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
       // program order = issue order (the scheduler otherwise sinks MFMAs below later reads and renames accumulators)
       __builtin_amdgcn_sched_barrier(0);
     });
+#ifdef CP25_ATTN_PROBE
+    ATTN_STAMP(probe_t, group_b ? 3 : 1);  // the phase's last MFMA issued
+    if (group_b && probe_on && (unsigned)(probe_t - a.probe_t0) < 32u) {
+      asm volatile("" : "+s"(probe_b2));  // its s_memtime has returned (the stamp above waited lgkmcnt(0))
+      probe_lds[(wave_u * 32 + probe_t - a.probe_t0) * 4 + 2] = probe_b2;
+    }
+#endif
     __builtin_amdgcn_s_setprio(0);
   };
   if (!group_b) {
     // group A: phase 2t MFMA, phase 2t+1 softmax(t+1) + V(t+1) staging
     auto step = [&](auto PAR, int t) __attribute__((always_inline)) {
       constexpr int par = decltype(PAR)::value;
+#ifdef CP25_ATTN_PROBE
+      probe_t = t;
+#endif
+      ATTN_STAMP(t, 0);  // (lab probe) MFMA phase opens
       mfma_phase(PAR, std::false_type{});
       __syncthreads();
+      ATTN_STAMP(t, 2);  // (lab probe) softmax phase opens
       if (t + 1 < ntiles) {
         if constexpr (kDmaV) {
           dma_tile(t + 1, std::integral_constant<int, par ^ 1>{});  // V(t+1): its buffer is free since the last barrier
@@ -843,6 +898,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
           load_tile(t + 2);
         }
       }
+      ATTN_STAMP(t, 3);  // (lab probe) softmax work done
       if constexpr (kDmaV) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // V(t+1) landed before the next P.V
       __syncthreads();
     };
@@ -855,6 +911,10 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
   } else {
     // group B: phase 2t softmax(t) + K(t+2) staging, phase 2t+1 MFMA
     auto step = [&](auto PAR, int t) __attribute__((always_inline)) {
+#ifdef CP25_ATTN_PROBE
+      probe_t = t;
+#endif
+      ATTN_STAMP(t, 0);  // (lab probe) softmax phase opens
       if constexpr (kDmaK) {
         if (t + 2 < ntiles) dma_tile(t + 2, PAR);  // buffer t & 1: K(t) was consumed in the last two phases
       } else {
@@ -864,12 +924,16 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
       if constexpr (!kDmaK) {
         if (t + 2 < ntiles) load_tile(t + 3);
       }
+      ATTN_STAMP(t, 1);  // (lab probe) softmax work done
       static_for<kAhead>([&](auto NC) __attribute__((always_inline)) { issue_pair(PAR, NC); });
       // a raw barrier behind a counted wait: the K(t+2) writes retire, the kAhead pairs' reads just issued stay in
       // flight across it (a __syncthreads() fence waited for them too, before the barrier, on the longer phase)
       asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(2 * kAhead) : "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+#ifdef CP25_ATTN_PROBE
+      if (probe_on && (unsigned)(t - a.probe_t0) < 32u) asm volatile("s_memtime %0" : "=s"(probe_b2)::"memory");
+#endif
       mfma_phase(PAR, std::true_type{});
       if constexpr (kDmaK) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K(t+2) landed before A reads it
       __syncthreads();
@@ -881,6 +945,18 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
     if (ntiles & 1) step(B0{}, ntiles - 1);
   }
 
+#ifdef CP25_ATTN_PROBE
+  if (probe_on) {  // this wave's stamps (it wrote them itself: its LDS accesses complete in order)
+    asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(probe_clk[2]), "=s"(probe_clk[3])::"memory");
+    for (int i = lane; i < 128; i += 64)
+      a.probe[((size_t)blockIdx.x * kWaves + wave_u) * 128 + i] = probe_lds[wave_u * 128 + i];
+    // after the per-tile stamps of all probe_wg workgroups: [wg][wave][4] loop-start / loop-end clocks
+    if (lane < 4)
+      a.probe[(size_t)a.probe_wg * kWaves * 128 + ((size_t)blockIdx.x * kWaves + wave_u) * 4 + lane] =
+          lane == 0 ? probe_clk[0] : lane == 1 ? probe_clk[1] : lane == 2 ? probe_clk[2] : probe_clk[3];
+  }
+#undef ATTN_STAMP
+#endif
   // ---- epilogue: lane holds O^T[16 db + 4 g + i][16 qh + c]: row q_row[qh], d = 16 db + 4 g + (0..3) ----
   if constexpr (kPersist) {
     store_block(blk_end - 1);
@@ -1401,6 +1477,17 @@ extern "C" int cp25_attn_cross_select(int form) {
   return prev;
 }
 
+#ifdef CP25_ATTN_PROBE
+// lab build only: where the next launches put their s_memtime stamps (nullptr: off)
+static unsigned long long* g_probe = nullptr;
+static int g_probe_t0 = 0, g_probe_wg = 0;
+extern "C" void cp25_attn_probe_set(unsigned long long* probe, int t0, int n_wg) {
+  g_probe = probe;
+  g_probe_t0 = t0;
+  g_probe_wg = n_wg;
+}
+#endif
+
 // fp8: 0 bf16; 1 = Q K^T on e4m3 q / k; 2 = also P.V on e5m2 P and the e4m3 v8t layout (v = v8t, v_strides unused)
 static int attn_launch(const void* q, const void* k, const void* v, void* o, int B, int H, int Lq, int Lk, int D,
                        const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
@@ -1478,6 +1565,11 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
   a.qn_eps = qn ? qn->qn_eps : 0.f;
   a.qn_scale = qn ? qn->qn_scale : 1.f;
   a.qn_row0 = 0;
+#ifdef CP25_ATTN_PROBE
+  a.probe = g_probe;
+  a.probe_t0 = g_probe_t0;
+  a.probe_wg = g_probe_wg;
+#endif
   const int64_t nwg = (int64_t)a.nqb * B * H * n_split;
   if (nwg > 0x7fffffff) return CP25_ERR_INVAL;
   const bool xk = Lk <= 4096;  // short-key launches (text cross-attention) get their own symbol in profiles
@@ -1643,7 +1735,7 @@ extern "C" int cp25_attn_fwd_prescaled_qnorm(const void* q, const void* k, const
   if (!q_norm_weight || ((uintptr_t)q_norm_weight & 15) || (!cos_tab) != (!sin_tab) || !(eps >= 0.f) ||
       !(q_scale > 0.f))
     return CP25_ERR_INVAL;
-  if ((((uintptr_t)cos_tab) | ((uintptr_t)sin_tab)) & 3) return CP25_ERR_INVAL;
+  if ((((uintptr_t)cos_tab) | ((uintptr_t)sin_tab)) & 15) return CP25_ERR_INVAL;  // read as f32x4 (as cp25_gemm_qkv)
   AttnArgs qn{};
   qn.qn_w = (const unsigned short*)q_norm_weight;
   qn.qn_cos = cos_tab;

@@ -16,7 +16,7 @@ Paths relative to cosmos_predict2/_src/predict2/networks/ unless stated:
   minimal_v4_dit.py:1567-1575      unpatchify
 Third-party numerics restated by their standard formulas (parity unpinned):
 TE RMSNorm (fp32 math, one rounding of (x*rstd)*w), TE fused RoPE (rotate-half, fp32), SDPA
-(fp32 softmax, bf16 output).
+(fp32 softmax, bf16 output; or, inside `flash_sdpa()`, the flash-attention forward's bf16-P numerics).
 
 Config: a dict with the DiTConfig field names (cosmos_predict2/net_config.py).
 Device-agnostic torch code: the tests run it on the CPU, and at full-geometry sizes that would take hours on host
@@ -107,9 +107,51 @@ def apply_rope(x: torch.Tensor, freqs: torch.Tensor) -> torch.Tensor:
     return x * c + rot * s
 
 
+# SDPA form of the bf16 restatement: "fp32p" (default) keeps the softmax weights P in fp32 through P.V (more exact
+# than any kernel the reference dispatches to); "flash" (inside `flash_sdpa()`) restates the flash-attention forward
+# those kernels run (networks/attention.py:119-178 dispatches to FlashAttention-3 / cuDNN SDPA / FlashAttention-2;
+# third-party, not vendored in the reference: FlashAttention-2, Dao 2023, Algorithm 1, as in its csrc
+# flash_fwd_kernel.h / softmax.h): key blocks of 128, a running row max m_j over the blocks seen so far, P_j =
+# exp2(S_j * scale * log2 e - m_j * scale * log2 e) in fp32, the row sum l over the UNROUNDED fp32 P, P_j rounded to
+# bf16 for the P.V product (fp32 accumulation), O rescaled by exp2 of the max change, O / l rounded once to bf16.
+# Parity unpinned (no fixture of those kernels exists here); it measures the bf16-P floor between two flash-class
+# implementations.
+_SDPA = ["fp32p"]
+
+
+@contextlib.contextmanager
+def flash_sdpa():
+    _SDPA.append("flash")
+    try:
+        yield
+    finally:
+        _SDPA.pop()
+
+
+def _flash_rows(qf: torch.Tensor, kf: torch.Tensor, vf: torch.Tensor, scale: float, blk: int = 128) -> torch.Tensor:
+    """FlashAttention-2 forward numerics on [B, H, q, D] fp32 q (bf16-valued) against [B, H, Lk, D] k / v: the key
+    blocks are processed in order with the running max (vectorised: the max seen through block j is the cumulative
+    max of the block maxima; the sequential rescales of O and l multiply to exp2(m_j - m_final) per block)."""
+    s = torch.matmul(qf, kf.transpose(-1, -2))  # raw scores, fp32
+    Lk = s.shape[-1]
+    nb = (Lk + blk - 1) // blk
+    pad = nb * blk - Lk
+    if pad:
+        s = F.pad(s, (0, pad), value=float("-inf"))
+    sb = s.view(*s.shape[:-1], nb, blk)
+    c = scale * math.log2(math.e)
+    m = torch.cummax(sb.amax(-1), dim=-1).values * c  # [.., q, nb] running max, log2 units
+    p = torch.exp2(sb * c - m[..., None])              # fp32 P of each block at its running max
+    w = torch.exp2(m - m[..., -1:])                    # rescale of block j to the final max
+    l = (p.sum(-1) * w).sum(-1, keepdim=True)          # row sum of the unrounded P
+    pw = (p.to(BF16).float() * w[..., None]).view(*s.shape[:-1], nb * blk)[..., :Lk]
+    return torch.matmul(pw, vf) / l
+
+
 def sdpa(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, chunk: int = 4096) -> torch.Tensor:
     """[B, S, H, D] bf16 -> [B, S, H*D] bf16 with fp32 softmax (query-chunked for memory: a chunk's fp32 scores stay
-    under ~16 GB, e.g. 384 queries at config 4's 163 800 keys)."""
+    under ~16 GB, e.g. 384 queries at config 4's 163 800 keys). Inside `flash_sdpa()`: the flash-attention numerics
+    (bf16 P for P.V, _flash_rows)."""
     B, Lq, H, D = q.shape
     chunk = max(128, min(chunk, (16 << 30) // (B * H * k.shape[1] * 4) // 128 * 128))
     kf = k.float().transpose(1, 2)
@@ -117,6 +159,9 @@ def sdpa(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, chunk: int = 4096) -
     outs = []
     for s0 in range(0, Lq, chunk):
         qf = q[:, s0 : s0 + chunk].float().transpose(1, 2)
+        if _SDPA[-1] == "flash" and act_dtype() == BF16:
+            outs.append(_flash_rows(qf, kf, vf, D ** -0.5).transpose(1, 2))
+            continue
         p = torch.softmax(torch.matmul(qf, kf.transpose(-1, -2)) * (D ** -0.5), dim=-1)
         outs.append(torch.matmul(p, vf).transpose(1, 2))
     o = torch.cat(outs, dim=1)

@@ -30,6 +30,16 @@ def test_no_lds_read_races(src):
 
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="hipcc not installed")
+def test_attention_m0_only_in_dma_asm():
+    """The attention's LDS-DMA asm writes M0 undeclared (reserved: the compiler never allocates it and ignores a
+    clobber of it); no compiler-emitted instruction of any attention kernel may name M0."""
+    rep = isa_check.check(os.path.join(CSRC, "attn_fwd.hip"))
+    assert rep
+    bad = {n: r["m0_uses"][:2] for n, r in rep.items() if r["m0_uses"]}
+    assert not bad, bad
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="hipcc not installed")
 def test_self_attention_loop_shape():
     rep = isa_check.check(os.path.join(CSRC, "attn_fwd.hip"), "attn_fwd_m16ILi0ELb1ELi1ELb0ELi0ELi0EE")
     (r,) = rep.values()  # the bench's kernel: self-attention, prescaled q, zero shift

@@ -134,6 +134,15 @@ def test_attention(device, Lk):
     qs = (q32 * c).to(BF16)
     hip_p = N.attn_fwd(qs, k, v, prescaled=True, norm_bounds=(bounds[0] * c * 1.01, bounds[1]))
     record(f"{kind}-attention, DiT default: q*c rounded once (cp25_attn_fwd_prescaled)", hip_p, ref, truth, 4e-3)
+    # like with like: the reference's real kernels (flash / cuDNN SDPA) round P to bf16 for P.V as these kernels do;
+    # the flash-class oracle (oracle.dit.flash_sdpa: FlashAttention-2's forward numerics, parity unpinned) is that
+    # reference, so hip-ref here is the bf16-P floor between two flash-class implementations
+    with odit.flash_sdpa():
+        ref_f = odit.sdpa(q, k, v).view(B, L, H, 128)
+    record(f"{kind}-attention vs flash-class reference (bf16 P), q rounded as the reference", hip, ref_f, truth, 4e-3,
+           note="reference = oracle.dit.flash_sdpa (FlashAttention-2 Algorithm 1 numerics)")
+    record(f"{kind}-attention vs flash-class reference (bf16 P), DiT default q*c", hip_p, ref_f, truth, 4e-3,
+           note="reference = oracle.dit.flash_sdpa (FlashAttention-2 Algorithm 1 numerics)")
 
 
 def test_block_gemms(device):

@@ -37,9 +37,11 @@ def test_embed_patches_own_gemm(device):
     mask = torch.ones(4, device=device)
     rows = N.patchify(xs, None, mask, None, tok0=0, hw=64, ld=128)
     geo = Geometry(T=4, Hp=8, Wp=8, tok0=0, n_tok=n, n_views=1)
-    own = net.embed_patches(rows.view(n, 1, 72), geo)
+    own = net.embed_patches(rows.view(n, 1, 72), geo, rows_k128=True)
     lib = F.linear(rows.contiguous(), net.sd["x_embedder.proj.1.weight"]).view(n, 1, -1)
     assert own.dtype == torch.bfloat16 and own.shape == lib.shape
     diff = (own.float() - lib.float()).abs()
     ulp = lib.float().abs().clamp_min(1e-3) * 2.0 ** -7
     assert (diff <= ulp).all(), diff.max().item()
+    # without the flag the same strided view takes the library GEMM over its 72 columns (never the padded storage)
+    assert torch.equal(net.embed_patches(rows.view(n, 1, 72), geo), lib)

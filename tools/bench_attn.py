@@ -16,6 +16,58 @@ import torch  # noqa: E402
 from cosmos_predict2 import _native as N  # noqa: E402
 
 
+def probe_report(T, clk=None):
+    """Phase anatomy of the attn_fwd_m16 loop from the lab probe's stamps T[wg][wave][tile][k] (s_memtime cycles).
+    Waves w and w + 4 share a SIMD. Per tile t: phase X = group A's MFMA phase (A0 -> A1: P.V(t), Q K^T(t+1)) beside
+    group B's softmax(t) (B0 -> B1), released at A2; phase Y = B's MFMA phase (B2 -> B3) beside A's softmax(t+1)
+    (A2 -> A3), released at the next A0. 68 MFMAs of 16 cycles = 1088 cycles of pipe per MFMA phase."""
+    import numpy as np
+    T = T.astype(np.int64)
+    A, Bw = T[:, 0:4], T[:, 4:8]
+    A0, A1, A2, A3 = (A[..., i] for i in range(4))
+    B0, B1, B2, B3 = (Bw[..., i] for i in range(4))
+    nxt = A0[:, :, 1:]
+    sl = (slice(None), slice(None), slice(0, -1))
+    r = {}
+
+    def m(x):
+        return round(float(np.median(x)), 1)
+    r["period"] = m(nxt - A0[sl])
+    r["X_len"] = m(A2[sl] - A0[sl])
+    r["Y_len"] = m(nxt - A2[sl])
+    r["A_mfma_span"] = m(A1 - A0)
+    r["B_mfma_span"] = m(B3 - B2)
+    r["B_softmax_span"] = m(B1 - B0)
+    r["A_softmax_span"] = m(A3 - A2)
+    r["X_overrun_softmax_after_mfma"] = m(B1 - A1)
+    r["Y_overrun_softmax_after_mfma"] = m(A3[sl] - B3[sl])
+    r["X_release_after_last"] = m(A2 - np.maximum(A1, B1))
+    r["Y_release_after_last"] = m(nxt - np.maximum(A3[sl], B3[sl]))
+    r["X_open_skew_B0_minus_A0"] = m(B0 - A0)
+    r["Y_open_skew_B2_minus_A2"] = m(B2 - A2)
+    idle = (nxt - A0[sl]) - (A1 - A0)[sl] - (B3 - B2)[sl]
+    r["mfma_idle_per_tile"] = m(idle)
+    # barrier anatomy over the whole workgroup: arrivals = the MFMA waves' last MFMA (A1 / B3) and the softmax waves'
+    # finished work (B1 / A3); release = the earliest opening stamp after the barrier (A2 / next A0)
+    arr_X = np.concatenate([A1, B1], axis=1)          # [wg, 8, tile]
+    arr_Y = np.concatenate([A3, B3], axis=1)[sl]
+    rel_X = np.minimum(A2.min(1), B2.min(1))          # [wg, tile]
+    rel_Y = np.minimum(A0.min(1), B0.min(1))[:, 1:]
+    r["X_release_after_last_of_8"] = m(rel_X - arr_X.max(1))
+    r["Y_release_after_last_of_8"] = m(rel_Y - arr_Y.max(1))
+    r["X_mfma_end_skew_over_simds"] = m(A1.max(1) - A1.min(1))  # group A's 4 MFMA waves
+    r["Y_mfma_end_skew_over_simds"] = m(B3.max(1) - B3.min(1))
+    r["X_last_arrival_is_mfma_wave"] = round(float((A1.max(1) >= B1.max(1)).mean()), 3)
+    r["Y_last_arrival_is_mfma_wave"] = round(float((B3[sl].max(1) >= A3[sl].max(1)).mean()), 3)
+    r["mfma_busy_share"] = round(float(np.median(((A1 - A0)[sl] + (B3 - B2)[sl]) / (nxt - A0[sl]))), 4)
+    if clk is not None:  # loop start / end: s_memtime (shader cycles) and s_memrealtime (100 MHz) per wave
+        clk = clk.astype(np.int64)
+        r["clock_ghz"] = round(float(np.median((clk[..., 2] - clk[..., 0]) / (clk[..., 3] - clk[..., 1]))) * 0.1, 4)
+        r["loop_cycles"] = m(clk[..., 2] - clk[..., 0])
+    r["note"] = "medians over workgroups x SIMDs x tiles, s_memtime cycles, each wait-form stamp ~40 cycles"
+    return r
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--L", type=int, default=109120)
@@ -43,6 +95,14 @@ def main():
                     help="with --bounded --prescaled: q stays the raw projection and the kernel applies the q RMSNorm "
                          "+ RoPE + prescale itself (cp25_attn_fwd_prescaled_qnorm, the DiT's default since round 4)")
     ap.add_argument("--lib", default="", help="lab build of libcp25.so to load instead of the in-tree one")
+    ap.add_argument("--probe", type=int, default=-1,
+                    help="with a -DCP25_ATTN_PROBE lab build: after the timing, one more launch records s_memtime "
+                         "stamps of tiles probe .. probe + 31 in the first --probe-wg workgroups (probe_report)")
+    ap.add_argument("--probe-wg", type=int, default=64)
+    ap.add_argument("--probe-dump", default="", help="save the raw probe stamps (.npy) here")
+    ap.add_argument("--force-online", action="store_true",
+                    help="with --bounded: pass a 10x larger q bound, so the online-max form runs on data the zero-shift "
+                         "form would take (the online form's cost on the same data)")
     a = ap.parse_args()
     if a.lib:
         N._LIB_PATH = a.lib
@@ -93,6 +153,9 @@ def main():
             pre["fp8_qk"] = (q8, k8)
             if a.fp8pv:
                 pre["fp8_v"] = N.cast_v_fp8t(v)
+    if a.force_online:
+        assert nb, "--force-online goes with --bounded"
+        nb = (nb[0] * 10.0, nb[1])
     # correctness of the loaded build on a small shape (ragged length) vs fp32 math
     gc = torch.Generator(device=dev).manual_seed(1)
     qc, kc, vc = (torch.randn(1, 1000, 2, 128, device=dev, generator=gc).to(torch.bfloat16) for _ in range(3))
@@ -114,9 +177,25 @@ def main():
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
     flop = 4.0 * a.B * a.H * a.L * Lk * 128
+    probe = None
+    if a.probe >= 0:
+        import ctypes
+        lib = N.load_library()
+        lib.cp25_attn_probe_set.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        buf_p = torch.zeros(a.probe_wg * 8 * (32 * 4 + 4), dtype=torch.int64, device=dev)
+        lib.cp25_attn_probe_set(ctypes.c_void_p(buf_p.data_ptr()), a.probe, a.probe_wg)
+        N.attn_fwd(q, k, v, out=o, n_split=ns, norm_bounds=nb, **pre)
+        torch.cuda.synchronize()
+        lib.cp25_attn_probe_set(None, 0, 0)
+        pb = buf_p.cpu().numpy()
+        if a.probe_dump:
+            import numpy as np
+            np.save(a.probe_dump, pb)
+        n_t = a.probe_wg * 8 * 128
+        probe = probe_report(pb[:n_t].reshape(a.probe_wg, 8, 32, 4), pb[n_t:].reshape(a.probe_wg, 8, 4))
     print(json.dumps({"kernel": "attn_fwd", "B": a.B, "H": a.H, "Lq": a.L, "Lk": Lk, "fused": a.fused,
-                      "zeros": a.zeros, "bounded": a.bounded, "prescaled": a.prescaled, "fp8qk": a.fp8qk, "fp8pv": a.fp8pv, "qnorm": a.qnorm, "normed": a.normed or a.bounded, "wrange": a.wrange, "split": ns or N.attn_plan(a.B, a.H, a.L, Lk), "iters": a.iters, "lib": os.path.basename(a.lib) or "libcp25.so", "ms": ms,
-                      "tflops": flop / ms / 1e9, "check_rel_l2": check}))
+                      "zeros": a.zeros, "bounded": a.bounded, "prescaled": a.prescaled, "fp8qk": a.fp8qk, "fp8pv": a.fp8pv, "qnorm": a.qnorm, "force_online": a.force_online, "normed": a.normed or a.bounded, "wrange": a.wrange, "split": ns or N.attn_plan(a.B, a.H, a.L, Lk), "iters": a.iters, "lib": os.path.basename(a.lib) or "libcp25.so", "ms": ms,
+                      "tflops": flop / ms / 1e9, "check_rel_l2": check, **({"probe": probe} if probe else {})}))
 
 
 if __name__ == "__main__":

@@ -130,8 +130,20 @@ def analyse(asm, name):
             if state[q] is None or new != state[q]:
                 state[q] = new
                 work.append(q)
+    # M0 outside the inline asm: the attention's DMA asm writes M0 without declaring it (a reserved register the
+    # compiler never allocates; a clobber of it is ignored), so any compiler-emitted instruction naming M0 in such a
+    # kernel (compiler-visible LDS-DMA, s_sendmsg, movrel indexing) could see or leave a value the asm relies on
+    m0_uses, in_asm = [], False
+    for l in lines:
+        s = l.strip()
+        if s.startswith(";;#ASMSTART"):
+            in_asm = True
+        elif s.startswith(";;#ASMEND"):
+            in_asm = False
+        elif not in_asm and s and not s.startswith((";", ".")) and re.search(r"(?<![\w])m0(?![\w])", s):
+            m0_uses.append(s)
     return {"races": [s for _, s in sorted(races)], "nops": nops, "inloop_nops": lnops, "m0_nops": m0nops,
-            "inloop_scratch": scr, "inloop_vmcnt0": vm0}
+            "inloop_scratch": scr, "inloop_vmcnt0": vm0, "m0_uses": m0_uses}
 
 
 def check(src, flt=""):
@@ -149,7 +161,8 @@ if __name__ == "__main__":
     for name, r in rep.items():
         bad += len(r["races"])
         print(f"{name[:72]:72s} vgpr {r.get('VGPRs')} spill {r.get('VGPRs Spill')} | in-loop scratch "
-              f"{r['inloop_scratch']} vmcnt(0) {r['inloop_vmcnt0']} | s_nop {r['nops']} (+{r['m0_nops']} M0) | LDS races {len(r['races'])}")
+              f"{r['inloop_scratch']} vmcnt(0) {r['inloop_vmcnt0']} | s_nop {r['nops']} (+{r['m0_nops']} M0) | LDS races {len(r['races'])}"
+              f" | compiler M0 uses {len(r['m0_uses'])}")
         for s in r["races"][:3]:
             print("    race:", s[:100])
     sys.exit(1 if bad else 0)

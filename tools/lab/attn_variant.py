@@ -5,7 +5,8 @@ usage: python tools/lab/attn_variant.py <name> <patch>[,<patch>...]  ->  tools/l
 patches: nostore (no O stores at block boundaries), nodma (no next-block Q copy), noqread (no Q read from LDS),
 nostagger (the Q copy at tile 0 in every workgroup; correct results), rowsum_first (correct results),
 prio_b_hold, prio_static_b (wave priority forms; correct results), ahead3, ahead4 (operand ring depth;
-correct results), hotload, noload (staging-load probes), none"""
+correct results), hotload, noload (staging-load probes), noexp, noreads (round-5 isolation builds), none
+DEFINES="-D..." adds compile definitions (e.g. -DCP25_ATTN_PROBE for the s_memtime probe)"""
 import os
 import subprocess
 import sys
@@ -55,8 +56,9 @@ PATCHES = {
     __builtin_amdgcn_s_setprio(1);
 """)],
     # operand ring depth of the MFMA phase (pairs read ahead of their MFMAs; ring = depth + 1); correct results
-    "ahead3": [("constexpr int kAhead = 2;", "constexpr int kAhead = 3;")],
-    "ahead4": [("constexpr int kAhead = 2;", "constexpr int kAhead = 4;")],
+    "ahead3": [("  constexpr int kAhead = online && !kPersist ? 3 : kAheadDefault;", "  constexpr int kAhead = !kPersist ? 3 : 2;")],
+    "ahead2": [("  constexpr int kAhead = online && !kPersist ? 3 : kAheadDefault;", "  constexpr int kAhead = 2;")],
+    "ahead4": [("  constexpr int kAhead = online && !kPersist ? 3 : kAheadDefault;", "  constexpr int kAhead = !kPersist ? 4 : 2;")],
     # staging-load probes of the self-attention loop (WRONG results): hotload = every tile's K/V load reads tile t & 1
     # (L2-resident bytes: the HBM part of the load latency gone); noload = no K/V loads after the prologue
     "hotload": [("      kt = t;\n", "      kt = t & 1;\n")],
@@ -71,6 +73,23 @@ PATCHES = {
       __syncthreads();
     };
     // pairs of tiles"""), ("      if (t + 2 < ntiles) load_tile(t + 3);\n", "      if (t < 0) load_tile(t + 3);\n")],
+    # round 5 isolation builds of the self-attention loop (WRONG results; read their probe spans, tools/bench_attn.py
+    # --probe, with DEFINES=-DCP25_ATTN_PROBE): noexp = P = bf16(S) without the v_exp (the softmax VALU minus 32 exp per
+    # wave and tile); noreads = the MFMA phase's 48 operand reads become empty asm (no LDS read latency or issue)
+    "noexp": [("          v[j] = static_cast<__bf16>(__builtin_amdgcn_exp2f(kPre ? sv : fmaf(sv, cs, -m_run[qh])));\n",
+               "          v[j] = static_cast<__bf16>(kPre ? sv : fmaf(sv, cs, -m_run[qh]));\n")],
+    "noreads": [('      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ring[n % kR]) : "v"(k_rd_lds), "i"(off));\n',
+                 '      asm volatile("; %0 %1 %2" : "=v"(ring[n % kR]) : "v"(k_rd_lds), "i"(off));\n'),
+                ('      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(v_rd_lds), "i"(off));\n'
+                 '      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(v_rd_lds), "i"(off + 16 * kVStride16));\n',
+                 '      asm volatile("; %0 %1 %2" : "=v"(lo) : "v"(v_rd_lds), "i"(off));\n'
+                 '      asm volatile("; %0 %1 %2" : "=v"(hi) : "v"(v_rd_lds), "i"(off + 16 * kVStride16));\n')],
+    # expdummy: the v_exp runs (its result kept alive) but P = bf16(S) as in noexp: noexp vs expdummy = the exp
+    # instruction's own cost, data equal; dmav: V staged by LDS-DMA in the zero-shift form too (correct results)
+    "expdummy": [("          v[j] = static_cast<__bf16>(__builtin_amdgcn_exp2f(kPre ? sv : fmaf(sv, cs, -m_run[qh])));\n",
+                  "          v[j] = static_cast<__bf16>(kPre ? sv : fmaf(sv, cs, -m_run[qh]));\n"
+                  "          { const float e_ = __builtin_amdgcn_exp2f(sv); asm volatile(\"\" ::\"v\"(e_)); }\n")],
+    "dmav": [("  constexpr bool kDmaV = kDmaK && online;\n", "  constexpr bool kDmaV = kDmaK;\n")],
     "none": [],
 }
 
@@ -87,6 +106,7 @@ def main():
     subprocess.check_call(["make", "-s", "-C", CSRC, "-j8"])
     flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-fhip-fp32-correctly-rounded-divide-sqrt",
              "-fno-honor-nans", "-fno-slp-vectorize", "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
+    flags += os.environ.get("DEFINES", "").split()  # e.g. DEFINES=-DCP25_ATTN_PROBE
     subprocess.check_call(["/opt/rocm/bin/hipcc", *flags, "-c", tmp, "-o", f"/tmp/attn_{name}.o"])
     others = [os.path.join(OBJ, f + ".o") for f in ("dit_ops", "fp8_ops", "gemm", "unipc", "vae_attn", "vae_ops")]
     out = os.path.join(ROOT, "tools", "lab", f"libcp25_{name}.so")
