@@ -616,7 +616,7 @@ class MinimalV1LVGDiT:
                       view_indices: Optional[torch.Tensor] = None, rows_k128: bool = False) -> torch.Tensor:
         """x_embedder (PatchEmbed Linear, minimal_v4_dit.py:846-913) of [n, Bx, 72] patch rows -> [n, Bx, D].
         rows_k128: the caller made patch_rows with patchify(ld=128), i.e. they are the [:, :72] view of a [n, 128]
-        buffer whose columns 72.. the kernel zeroed; the own GEMM then multiplies the whole padded rows (K = 128)."""
+        buffer whose columns 72.. the kernel zeroed; the own GEMM then multiplies the whole padded rows (K = 128).
         Multi-view nets also concatenate a view embedding as input channels
         (prepare_embedded_sequence, multiview_dit.py:462-490); those channels are constant over a view, so
         their patch features (c, p1, p2) fold into one per-view bias: y = rows W72^T + e_v Wv^T, summed
