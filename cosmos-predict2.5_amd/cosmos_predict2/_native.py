@@ -97,6 +97,7 @@ SIGNATURES = {
     "cp25_rms_norm_silu": [_P, _P, _P, _I64, _I, _I, _P],
     "cp25_conv3d_select": [_I],
     "cp25_attn_cross_select": [_I],
+    "cp25_gemm_select": [_I],
     "cp25_softmax_rows": [_P, _I64, _I, _I64, _F, _P, _I64, _P],
     "cp25_vae_attn": [_P, _I64, _I64, _P, _I64, _I64, _P, _I64, _I64, _P, _I64, _I64, _I, _I, _I, _I, _F, _P, _I64,
                       _P],
@@ -312,6 +313,14 @@ def attn_cross_select(form: int) -> int:
     0 = one workgroup per query block (A/B and tests; bit-identical). Returns the previous form."""
     rc = load_library().cp25_attn_cross_select(int(form))
     _check("cp25_attn_cross_select", min(rc, 0))
+    return rc
+
+
+def gemm_select(form: int) -> int:
+    """cp25_gemm_select: the bf16 block-GEMM kernel form, 0 = gemm_nt_8ph (8 waves of 128 x 64), 1 = gemm_nt_4w (4
+    waves of 128 x 128); bit-identical (the same MFMA chains in the same K order). Returns the previous form."""
+    rc = load_library().cp25_gemm_select(int(form))
+    _check("cp25_gemm_select", min(rc, 0))
     return rc
 
 
