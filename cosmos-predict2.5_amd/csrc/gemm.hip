@@ -266,8 +266,10 @@ constexpr int kBuf8 = 4 * kHalf;      // A0 A1 B0 B1
 constexpr int kGeluE0 = 111, kGeluNE = 19;
 constexpr int kGeluTab = 2 * kGeluNE * 128;  // entries
 __device__ __forceinline__ int gelu_tab_index(unsigned u) {  // u: bf16 bits; -1 outside the table
-  const unsigned e = ((u >> 7) & 0xffu) - (unsigned)kGeluE0;
-  return e < (unsigned)kGeluNE ? (int)((u >> 15) * (kGeluNE * 128) + e * 128 + (u & 127u)) : -1;
+  // (exponent e, mantissa m) of one sign are the contiguous bit range [kGeluE0 128, (kGeluE0 + kGeluNE) 128): the
+  // index is (u & 0x7fff) - kGeluE0 128 + sign kGeluNE 128 (3 VALU instead of 6 for the exponent / mantissa split)
+  const unsigned m = (u & 0x7fffu) - (unsigned)(kGeluE0 * 128);
+  return m < (unsigned)(kGeluNE * 128) ? (int)(m + (u >> 15) * (kGeluNE * 128)) : -1;
 }
 
 template <int kEpi, int kES = 2>
@@ -533,18 +535,7 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
                 const f32x4_t as = *reinterpret_cast<const f32x4_t*>(sc + mq * 128 + wr * 64 + 16 * i + 4 * fg);
                 a = a * as[r] * sc[256 + nq * 128 + wc * 32 + 16 * j + fr];
               }
-              if constexpr (kEpi == CP25_EPI_GELU) {
-                const unsigned short u = f2bf(a);
-                const int ti = gelu_tab_index(u);
-                unsigned short g = reinterpret_cast<const unsigned short*>(smem + 2 * kBuf8)[ti < 0 ? 0 : ti];
-                if (__builtin_expect(__any(ti < 0), 0)) {
-                  const unsigned short gs = f2bf(gelu_exact(bf2f(u)));
-                  g = ti < 0 ? gs : g;
-                }
-                stj[j][(mq * 128 + 16 * i + r) * 256 + nq * 128] = g;
-              } else {
-                stj[j][(mq * 128 + 16 * i + r) * 256 + nq * 128] = f2bf(rbf(a));
-              }
+              stj[j][(mq * 128 + 16 * i + r) * 256 + nq * 128] = f2bf(rbf(a));  // (GELU: applied after the readback)
             }
     // (after the accumulators are in the LDS: their registers hold the gate chunks)
     if constexpr (kEpi == CP25_EPI_RES) {
@@ -658,6 +649,34 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
       issue_first_two();
     }
     __builtin_amdgcn_sched_barrier(0);  // the DMAs are queued ahead of the stores (the counts above rely on it)
+    if constexpr (kEpi == CP25_EPI_GELU) {
+      // the GELU on the read-back bf16 products, by table (its own LDS region, untouched by the DMA just queued, so the
+      // lookups run under that DMA's latency instead of in the C staging before it); one wave-wide test per 8-element
+      // chunk for an input outside the table, which then takes gelu_erf
+      const unsigned short* tab = reinterpret_cast<const unsigned short*>(smem + 2 * kBuf8);
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        u32x4 o;
+        bool miss = false;
+#pragma unroll
+        for (int w2 = 0; w2 < 4; ++w2) {
+          const unsigned u0 = cv[it][w2] & 0xffffu, u1 = cv[it][w2] >> 16;
+          const int t0 = gelu_tab_index(u0), t1 = gelu_tab_index(u1);
+          miss |= (t0 | t1) < 0;
+          o[w2] = (unsigned)tab[t0 < 0 ? 0 : t0] | ((unsigned)tab[t1 < 0 ? 0 : t1] << 16);
+        }
+        if (__builtin_expect(__any(miss), 0)) {
+#pragma unroll
+          for (int w2 = 0; w2 < 4; ++w2) {
+            const unsigned u0 = cv[it][w2] & 0xffffu, u1 = cv[it][w2] >> 16;
+            const unsigned g0 = gelu_tab_index(u0) < 0 ? f2bf(gelu_exact(bf2f((unsigned short)u0))) : (o[w2] & 0xffffu);
+            const unsigned g1 = gelu_tab_index(u1) < 0 ? f2bf(gelu_exact(bf2f((unsigned short)u1))) : (o[w2] >> 16);
+            o[w2] = g0 | (g1 << 16);
+          }
+        }
+        cv[it] = o;
+      }
+    }
     if constexpr (kEpi == CP25_EPI_HNORM) {
       // lanes 16 h .. 16 h + 15 of a 32-lane row hold head h's 128 columns, lane li = ch & 15 the 8 columns 8 li ..:
       // cp25_head_rmsnorm_rope's item layout, so its butterfly over 16 lanes is this one (runs under the DMA above)
