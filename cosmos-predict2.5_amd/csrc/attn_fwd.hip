@@ -263,6 +263,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
   // the phase's closing stamp.
   __shared__ unsigned long long probe_lds[kWaves * 32 * 4];
   unsigned long long probe_clk[4] = {0, 0, 0, 0};  // s_memtime, s_memrealtime (100 MHz) at the loop's start and end
+  unsigned probe_resc = 0;                          // online form: tiles t > 0 whose row max moved a shift (the rescale)
   const bool probe_on = !kPersist && kTail == 0 && a.probe != nullptr && (int)blockIdx.x < a.probe_wg;
   int probe_t = -1;
   unsigned long long probe_b2 = 0;
@@ -706,6 +707,9 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
         mx[qh] = kPre ? x : fmaf(x, cs, -m_run[qh]);
       }
       if (__builtin_expect(t == 0 || __any(fmaxf(mx[0], mx[1]) > kLazy), 0)) {
+#ifdef CP25_ATTN_PROBE
+        probe_resc += t > 0;
+#endif
 #pragma unroll
         for (int qh = 0; qh < 2; ++qh) mx[qh] = group4_max(mx[qh]);  // the whole row's (the shift is per row)
 #pragma unroll
@@ -950,10 +954,11 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
     asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(probe_clk[2]), "=s"(probe_clk[3])::"memory");
     for (int i = lane; i < 128; i += 64)
       a.probe[((size_t)blockIdx.x * kWaves + wave_u) * 128 + i] = probe_lds[wave_u * 128 + i];
-    // after the per-tile stamps of all probe_wg workgroups: [wg][wave][4] loop-start / loop-end clocks
-    if (lane < 4)
-      a.probe[(size_t)a.probe_wg * kWaves * 128 + ((size_t)blockIdx.x * kWaves + wave_u) * 4 + lane] =
-          lane == 0 ? probe_clk[0] : lane == 1 ? probe_clk[1] : lane == 2 ? probe_clk[2] : probe_clk[3];
+    // after the per-tile stamps of all probe_wg workgroups: [wg][wave][8] loop-start / loop-end clocks, rescales
+    if (lane < 5)
+      a.probe[(size_t)a.probe_wg * kWaves * 128 + ((size_t)blockIdx.x * kWaves + wave_u) * 8 + lane] =
+          lane == 0 ? probe_clk[0] : lane == 1 ? probe_clk[1] : lane == 2 ? probe_clk[2] : lane == 3 ? probe_clk[3]
+                                                                                                    : probe_resc;
   }
 #undef ATTN_STAMP
 #endif

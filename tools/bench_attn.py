@@ -64,6 +64,8 @@ def probe_report(T, clk=None):
         clk = clk.astype(np.int64)
         r["clock_ghz"] = round(float(np.median((clk[..., 2] - clk[..., 0]) / (clk[..., 3] - clk[..., 1]))) * 0.1, 4)
         r["loop_cycles"] = m(clk[..., 2] - clk[..., 0])
+        if clk.shape[-1] > 4:
+            r["rescale_tiles_per_wave"] = round(float(clk[..., 4].mean()), 2)
     r["note"] = "medians over workgroups x SIMDs x tiles, s_memtime cycles, each wait-form stamp ~40 cycles"
     return r
 
@@ -182,7 +184,7 @@ def main():
         import ctypes
         lib = N.load_library()
         lib.cp25_attn_probe_set.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
-        buf_p = torch.zeros(a.probe_wg * 8 * (32 * 4 + 4), dtype=torch.int64, device=dev)
+        buf_p = torch.zeros(a.probe_wg * 8 * (32 * 4 + 8), dtype=torch.int64, device=dev)
         lib.cp25_attn_probe_set(ctypes.c_void_p(buf_p.data_ptr()), a.probe, a.probe_wg)
         N.attn_fwd(q, k, v, out=o, n_split=ns, norm_bounds=nb, **pre)
         torch.cuda.synchronize()
@@ -192,7 +194,7 @@ def main():
             import numpy as np
             np.save(a.probe_dump, pb)
         n_t = a.probe_wg * 8 * 128
-        probe = probe_report(pb[:n_t].reshape(a.probe_wg, 8, 32, 4), pb[n_t:].reshape(a.probe_wg, 8, 4))
+        probe = probe_report(pb[:n_t].reshape(a.probe_wg, 8, 32, 4), pb[n_t:].reshape(a.probe_wg, 8, 8))
     print(json.dumps({"kernel": "attn_fwd", "B": a.B, "H": a.H, "Lq": a.L, "Lk": Lk, "fused": a.fused,
                       "zeros": a.zeros, "bounded": a.bounded, "prescaled": a.prescaled, "fp8qk": a.fp8qk, "fp8pv": a.fp8pv, "qnorm": a.qnorm, "force_online": a.force_online, "normed": a.normed or a.bounded, "wrange": a.wrange, "split": ns or N.attn_plan(a.B, a.H, a.L, Lk), "iters": a.iters, "lib": os.path.basename(a.lib) or "libcp25.so", "ms": ms,
                       "tflops": flop / ms / 1e9, "check_rel_l2": check, **({"probe": probe} if probe else {})}))

@@ -90,6 +90,20 @@ PATCHES = {
                   "          v[j] = static_cast<__bf16>(kPre ? sv : fmaf(sv, cs, -m_run[qh]));\n"
                   "          { const float e_ = __builtin_amdgcn_exp2f(sv); asm volatile(\"\" ::\"v\"(e_)); }\n")],
     "dmav": [("  constexpr bool kDmaV = kDmaK && online;\n", "  constexpr bool kDmaV = kDmaK;\n")],
+    # vsum: the row sums as fp32 VALU adds of the unrounded P (FlashAttention's form) in two per-lane partial chains,
+    # reduced over the row's 4 lanes at the end, instead of 4 MFMAs per tile against an all-ones row (different
+    # rounding: not bit-identical to the product)
+    "vsum": [("""#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) lsum[qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones8, pb[ks][qh], lsum[qh], 0, 0, 0);
+""", ""),
+             ("          v[j] = static_cast<__bf16>(__builtin_amdgcn_exp2f(kPre ? sv : fmaf(sv, cs, -m_run[qh])));\n",
+              "          const float e_ = __builtin_amdgcn_exp2f(kPre ? sv : fmaf(sv, cs, -m_run[qh]));\n"
+              "          lsum[qh][ks] += e_;\n"
+              "          v[j] = static_cast<__bf16>(e_);\n"),
+             ("    const float l_tot = lsum[qh][0];\n", "    const float l_tot = group4_sum(lsum[qh][0] + lsum[qh][1]);\n"),
+             ("      const float inv = 1.f / lsum[qh][0];\n", "      const float inv = 1.f / group4_sum(lsum[qh][0] + lsum[qh][1]);\n")],
     "none": [],
 }
 
