@@ -80,6 +80,9 @@ SIGNATURES = {
     "cp25_copy_rows": [_P, _I64, _P, _I64, _I64, _I64, _P],
     "cp25_gelu": [_P, _I64, _P],
     "cp25_gemm_epi": [_P, _I64, _P, _I64, _P, _I64, _I, _I, _I, _I, _P],
+    "cp25_gemm_f32": [_P, _I64, _I64, _P, _I64, _I64, _P, _I64, _I64, _P, _I64, _I64, _I, _I, _I, _I, _I, _P, _I64,
+                      _P],
+    "cp25_gemm_f32_workspace_floats": [_I, _I, _I, _I],
     "cp25_gemm_hnorm": [_P, _I64, _P, _I64, _P, _I64, _I, _I, _I, _P, _F, _F, _P],
     "cp25_gemm_qkv": [_P, _I64, _P, _I64, _P, _I64, _I, _I, _I, _I, _I, _P, _P, _P, _I, _F, _P],
     "cp25_gemm_res": [_P, _I64, _P, _I64, _P, _I64, _I, _I, _I, _P, _I64, _I64, _P, _I64, _I64, _I, _I64, _I64, _P],
@@ -130,6 +133,7 @@ def load_library() -> ctypes.CDLL:
         if argtypes is not None:
             fn.argtypes = argtypes
         fn.restype = {"cp25_attn_workspace_bytes": ctypes.c_size_t, "cp25_attn_tail_workspace_bytes": ctypes.c_size_t, "cp25_v_fp8t_bytes": ctypes.c_int64,
+                      "cp25_gemm_f32_workspace_floats": ctypes.c_int64,
                       "cp25_attn_kernel": ctypes.c_char_p,
                       "cp25_vae_attn_workspace_bytes": ctypes.c_int64}.get(name, ctypes.c_int)
     _lib = lib
@@ -499,6 +503,50 @@ def gemm_epi(a: torch.Tensor, w: torch.Tensor, epilogue: int = EPI_NONE, out: Op
     rc = lib.cp25_gemm_epi(_ptr(a), a.stride(0), _ptr(w), w.stride(0), _ptr(out), out.stride(0), M, N, K, int(epilogue),
                            _stream(a.device))
     _check("cp25_gemm_epi", rc)
+    return out
+
+
+ACT_NONE, ACT_SILU = 0, 1
+
+
+def gemm_f32(a: torch.Tensor, w: torch.Tensor, add: Optional[torch.Tensor] = None, act: int = ACT_NONE,
+             out: Optional[torch.Tensor] = None, split_k: bool = True) -> torch.Tensor:
+    """out = act(a w^T + add) in fp32 (cp25_gemm_f32): the fp32 conditioning linears (t-embedding, AdaLN-LoRA, final
+    layer). a [M, K] with w [N, K], or batched a [nb, M, K] with w [nb, N, K] (a's entries may be strided views, e.g.
+    column blocks of one wider matrix). add: broadcastable to the output ([N] bias, [M, N] or [nb, M, N]; strides
+    taken as given, stride-0 dimensions broadcast). K % 32 == 0. split_k=False: no K split whatever the shape, so
+    every output row's sum is independent of M (token rows of a context-parallel shard)."""
+    lib = load_library()
+    if a.dtype != torch.float32 or w.dtype != torch.float32:
+        raise ValueError("gemm_f32 expects fp32 operands")
+    if a.dim() != w.dim() or a.dim() not in (2, 3) or a.shape[-1] != w.shape[-1] or a.stride(-1) != 1 \
+            or w.stride(-1) != 1 or (a.dim() == 3 and a.shape[0] != w.shape[0]):
+        raise ValueError(f"gemm_f32 shapes a{tuple(a.shape)} w{tuple(w.shape)}: need [(nb,) M, K] x [(nb,) N, K]")
+    a3 = a if a.dim() == 3 else a.unsqueeze(0)
+    w3 = w if w.dim() == 3 else w.unsqueeze(0)
+    nb, M, K = a3.shape
+    N = w3.shape[1]
+    if out is None:
+        out = torch.empty((nb, M, N), dtype=torch.float32, device=a.device)
+        if a.dim() == 2:
+            out = out[0]
+    o3 = out if out.dim() == 3 else out.unsqueeze(0)
+    if tuple(o3.shape) != (nb, M, N) or o3.stride(2) != 1 or out.dtype != torch.float32:
+        raise ValueError(f"gemm_f32 out {tuple(out.shape)} != ({nb}, {M}, {N}) fp32")
+    r, ldr, sr = None, 0, 0
+    if add is not None:
+        if add.dtype != torch.float32:
+            raise ValueError("gemm_f32 addend must be fp32")
+        r3 = add.expand(nb, M, N)
+        if r3.stride(2) != 1:
+            raise ValueError("gemm_f32 addend must be contiguous along N")
+        r, ldr, sr = r3, r3.stride(1), r3.stride(0)
+    nws = lib.cp25_gemm_f32_workspace_floats(M, N, K, nb) if split_k and K % 32 == 0 else 0
+    ws = torch.empty(nws, dtype=torch.float32, device=a.device) if nws else None
+    rc = lib.cp25_gemm_f32(_ptr(a3), a3.stride(1), a3.stride(0), _ptr(w3), w3.stride(1), w3.stride(0), _ptr(r), ldr, sr,
+                           _ptr(o3), o3.stride(1), o3.stride(0), M, N, K, nb, int(act), _ptr(ws), nws,
+                           _stream(a.device))
+    _check("cp25_gemm_f32", rc)
     return out
 
 

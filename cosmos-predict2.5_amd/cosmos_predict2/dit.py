@@ -444,6 +444,12 @@ class MinimalV1LVGDiT:
         self.w_ada2 = torch.stack([p[f"blocks.{i}.adaln_modulation_{m}.2.weight"]
                                    for i in range(cfg.num_blocks) for m in ("self_attn", "cross_attn", "mlp")], 0).float()
         self.w_final = p["final_layer.linear.weight"].float()
+        # fp32 copies of the conditioning weights (the reference runs these layers under fp32 autocast)
+        self.w_t1 = p["t_embedder.1.linear_1.weight"].float()
+        self.w_t2 = p["t_embedder.1.linear_2.weight"].float()
+        self.w_f1 = p["final_layer.adaln_modulation.1.weight"].float()
+        self.w_f2 = p["final_layer.adaln_modulation.2.weight"].float()
+        self._xproj_wb = None
         self.refresh_norm_bounds()
         self._rope_cache.clear()
         if D % 512:
@@ -501,18 +507,40 @@ class MinimalV1LVGDiT:
         """crossattn_emb [B, Lctx, proj_in] -> per-block cross-attention K/V (normed)."""
         cfg = self.cfg
         p = self.sd
-        ctx = crossattn_emb.to(device=self.device, dtype=BF16)
+        B, Lc, c_in = crossattn_emb.shape
         if cfg.use_crossattn_projection:
-            ctx = F.linear(ctx, p["crossattn_proj.0.weight"], p["crossattn_proj.0.bias"]).contiguous()
-            N.gelu_(ctx)
-        B, Lc, _ = ctx.shape
+            w, bias = p["crossattn_proj.0.weight"], p["crossattn_proj.0.bias"]
+            kp = (c_in + 1 + 63) // 64 * 64
+            if self.block_gemm == "own" and N.gemm_supported(w.shape[0], kp):
+                # crossattn_proj = Linear + bias + exact GELU (minimal_v4_dit.py:1430-1434, applied at :1604) on the
+                # hand-written GEMM: the bias rides as one more K column (a' = [emb | 1 | 0], w' = [w | bias | 0]), so
+                # it enters the fp32 accumulator before the product's one bf16 rounding, as the library's bias
+                # epilogue adds it; EPI_GELU then applies the GELU to the rounded sum (cp25_gelu's arithmetic).
+                if self._xproj_wb is None or self._xproj_wb.shape[1] != kp:
+                    wb = torch.zeros((w.shape[0], kp), dtype=BF16, device=self.device)
+                    wb[:, :c_in] = w
+                    wb[:, c_in] = bias
+                    self._xproj_wb = wb
+                a = torch.zeros((B * Lc, kp), dtype=BF16, device=self.device)
+                a[:, :c_in] = crossattn_emb.reshape(B * Lc, c_in)
+                a[:, c_in] = 1.0
+                ctx = N.gemm_epi(a, self._xproj_wb, epilogue=N.EPI_GELU)
+                del a
+            else:
+                ctx = F.linear(crossattn_emb.to(device=self.device, dtype=BF16), w, bias).reshape(B * Lc, -1).contiguous()
+                N.gelu_(ctx)
+        else:
+            ctx = crossattn_emb.to(device=self.device, dtype=BF16).reshape(B * Lc, c_in).contiguous()
         H, hd = cfg.num_heads, cfg.head_dim
         ks, vs = [], []
         for i in range(cfg.num_blocks):
-            k = F.linear(ctx, p[f"blocks.{i}.cross_attn.k_proj.weight"]).contiguous()
-            N.head_rmsnorm_rope(k.view(B * Lc, H * hd), n_rows=B * Lc, B=1, H=H, head_off=0,
+            # cross-attention k/v projections (minimal_v4_dit.py:401-404) of the text context, once per prompt
+            wk, wv = p[f"blocks.{i}.cross_attn.k_proj.weight"], p[f"blocks.{i}.cross_attn.v_proj.weight"]
+            own = self.block_gemm == "own" and N.gemm_supported(wk.shape[0], wk.shape[1])
+            k = N.gemm_epi(ctx, wk) if own else F.linear(ctx, wk)
+            N.head_rmsnorm_rope(k, n_rows=B * Lc, B=1, H=H, head_off=0,
                                 weight=p[f"blocks.{i}.cross_attn.k_norm.weight"])
-            v = F.linear(ctx, p[f"blocks.{i}.cross_attn.v_proj.weight"]).contiguous()
+            v = N.gemm_epi(ctx, wv) if own else F.linear(ctx, wv)
             ks.append(k.view(B, Lc, H, hd))
             vs.append(v.view(B, Lc, H, hd))
         return ContextCache(B=B, k=ks, v=vs)
@@ -579,8 +607,9 @@ class MinimalV1LVGDiT:
         expo = expo / (half - 0.0)
         arg = t_B_T.flatten().float()[:, None] * torch.exp(expo)[None, :]
         sincos = torch.cat([torch.cos(arg), torch.sin(arg)], dim=-1).view(B, T, D)
-        h = F.silu(F.linear(sincos, p["t_embedder.1.linear_1.weight"].float()))
-        lora = F.linear(h, p["t_embedder.1.linear_2.weight"].float())  # [B, T, 3D]
+        # every fp32 linear below on cp25_gemm_f32 (fp32 MFMA): TimestepEmbedding (minimal_v4_dit.py:727-788)
+        h = N.gemm_f32(sincos.view(B * T, D), self.w_t1, act=N.ACT_SILU)
+        lora = N.gemm_f32(h, self.w_t2).view(B, T, 3 * D)
         if cfg.action_dim:
             if action is None:
                 raise ValueError("this action-conditioned net needs `action`")
@@ -593,11 +622,15 @@ class MinimalV1LVGDiT:
         emb = ((xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-6)) * p["t_embedding_norm.weight"].float())
         se = F.silu(emb)  # [B, T, D]
         nb3 = 3 * cfg.num_blocks
-        a1 = F.linear(se, self.w_ada1).view(B * T, nb3, -1).transpose(0, 1)  # [nb3, BT, A]
-        a2 = torch.bmm(a1, self.w_ada2.transpose(1, 2))  # [nb3, BT, 3D]
-        mods = (a2 + lora.view(1, B * T, 3 * D)).view(cfg.num_blocks, 3, B, T, 3 * D).to(BF16)
-        f1 = F.linear(se, p["final_layer.adaln_modulation.1.weight"].float())
-        f2 = F.linear(f1, p["final_layer.adaln_modulation.2.weight"].float()) + lora[..., : 2 * D]
+        se = se.reshape(B * T, D)
+        lora2 = lora.view(B * T, 3 * D)
+        # AdaLN-LoRA of every block sub-layer (minimal_v4_dit.py:1136-1154): the 3 nb Linear(D, A) as one GEMM, the
+        # 3 nb Linear(A, 3D) as one batched GEMM over the column blocks of its output, + the LoRA term in the epilogue
+        a1 = N.gemm_f32(se, self.w_ada1).view(B * T, nb3, -1).transpose(0, 1)  # [nb3, BT, A]
+        a2 = N.gemm_f32(a1, self.w_ada2, add=lora2)  # [nb3, BT, 3D]
+        mods = a2.view(cfg.num_blocks, 3, B, T, 3 * D).to(BF16)
+        f1 = N.gemm_f32(se, self.w_f1)
+        f2 = N.gemm_f32(f1, self.w_f2, add=lora2[:, : 2 * D]).view(B, T, 2 * D)
         shift_f, scale_f = f2.chunk(2, dim=-1)
         return mods, shift_f, scale_f
 
@@ -842,7 +875,7 @@ class MinimalV1LVGDiT:
                 yield i
         # ---- final layer (fp32 autocast): x + g*y -> LN -> modulate -> Linear(D -> 64)
         xf = N.final_ln_mod(x, shift_f, scale_f, y=y, gate=gate_prev, **common)
-        out = F.linear(xf.view(n * B, D), self.w_final)
+        out = N.gemm_f32(xf.view(n * B, D), self.w_final, split_k=False)  # rows independent of the shard size
         return out.view(n, B, -1)
 
     def _cross_attention(self, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, o: torch.Tensor, geo: Geometry,

@@ -234,6 +234,26 @@ int cp25_copy_rows(const void* src, int64_t src_stride, void* dst, int64_t dst_s
  * Replaces: GPT2FeedForward activation, minimal_v4_dit.py:249-254. */
 int cp25_gelu(void* x, int64_t n, hipStream_t stream);
 
+/* fp32 linear layers: C[b][M, N] = act(A[b][M, K] W[b][N, K]^T + R[b][M, N]) in fp32 on v_mfma_f32_16x16x4_f32 (fp32
+ * operands, products and sums). Batch entry b's matrices at a + b * a_batch_stride (etc.); A / W / C row-major with
+ * leading dims lda / ldw / ldc (floats; lda, ldw and the A / W batch strides multiples of 4, a / w 16-B aligned). R
+ * (NULL: none) at r + b * r_batch_stride + row * ldr + col: ldr = 0 is a bias vector, r_batch_stride = 0 one addend
+ * for every entry. act 0: none, 1: SiLU (x * sigmoid(x)) after the addend. K % 32 == 0 (-95 otherwise), any M / N,
+ * batch <= 65535. Launches with few tiles (the 62-row conditioning GEMMs) split K over several workgroups when a
+ * workspace of cp25_gemm_f32_workspace_floats(M, N, K, batch) floats is given (partial sums, then a second pass adds
+ * them in slice order, then R and act); with none, or a smaller one, one slice runs. The slice plan depends only on
+ * the shape: a given shape always sums in the same order. Without a workspace an output row's sum does not depend on
+ * M (the final linear passes none: a context-parallel shard's rows equal the whole sequence's, bit for bit).
+ * Replaces the fp32 F.linear calls of the reference's fp32 conditioning (use_wan_fp32_strategy,
+ * minimal_v4_dit.py): TimestepEmbedding linear_1 + SiLU and linear_2 (:727-788), the blocks' AdaLN-LoRA
+ * modulation Linear(D, A) / Linear(A, 3D) + the LoRA term (:1136-1154; all 3 x num_blocks sub-layers as one GEMM and
+ * one batched GEMM), the final layer's AdaLN (:974-991) and its Linear(D, p p C) (:993-995). */
+int cp25_gemm_f32(const float* a, int64_t lda, int64_t a_batch_stride, const float* w, int64_t ldw,
+                  int64_t w_batch_stride, const float* r, int64_t ldr, int64_t r_batch_stride, float* c, int64_t ldc,
+                  int64_t c_batch_stride, int M, int N, int K, int batch, int act, float* workspace,
+                  int64_t workspace_floats, hipStream_t stream);
+int64_t cp25_gemm_f32_workspace_floats(int M, int N, int K, int batch);
+
 /* ---------------------------------------------------------------- block projections (GEMM + epilogue)
  * C[M, N] = epi(A[M, K] W[N, K]^T): A, W, C bf16 row-major with leading dims lda / ldw / ldc (elements,
  * multiples of 8, pointers 16-B aligned), fp32 accumulation, one bf16 rounding of the product.

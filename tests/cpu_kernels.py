@@ -107,6 +107,18 @@ def gemm_epi(a, w, epilogue=N.EPI_NONE, out=None):
     return out
 
 
+def gemm_f32(a, w, add=None, act=N.ACT_NONE, out=None, split_k=True):
+    y = torch.matmul(a, w.transpose(-1, -2))
+    if add is not None:
+        y = y + add
+    if act == N.ACT_SILU:
+        y = F.silu(y)
+    if out is None:
+        return y
+    out.copy_(y)
+    return out
+
+
 def gemm_res(a, w, x, x_st, x_sb, gate, *, B, tok0, hw, out=None):
     M, Nn = a.shape[0], w.shape[0]
     n = M // B
@@ -188,7 +200,7 @@ def vae_attn(q, k, v, out=None, scale=None):
 
 
 _FUNCS = dict(conv3d=conv3d, rms_norm_silu=rms_norm_silu, vae_attn=vae_attn, ln_mod=ln_mod, final_ln_mod=final_ln_mod, head_rmsnorm_rope=head_rmsnorm_rope, copy_rows=copy_rows,
-              attn_fwd=attn_fwd, attn_kernel_name=attn_kernel_name, gemm_epi=gemm_epi, gemm_res=gemm_res,
+              attn_fwd=attn_fwd, attn_kernel_name=attn_kernel_name, gemm_epi=gemm_epi, gemm_f32=gemm_f32, gemm_res=gemm_res,
               gemm_hnorm=gemm_hnorm, gemm_qkv=gemm_qkv, gelu_=gelu_)
 
 
