@@ -449,7 +449,8 @@ class MinimalV1LVGDiT:
         self.w_t2 = p["t_embedder.1.linear_2.weight"].float()
         self.w_f1 = p["final_layer.adaln_modulation.1.weight"].float()
         self.w_f2 = p["final_layer.adaln_modulation.2.weight"].float()
-        self._xproj_wb = None
+        self._bias_w = {}  # padded [w | bias | 0] copies for _bias_linear, per weight name
+        self._embed_f32 = None  # multi-view patch embedding: fp32 weight padded to K = 96, view-channel fold
         self.refresh_norm_bounds()
         self._rope_cache.clear()
         if D % 512:
@@ -509,25 +510,12 @@ class MinimalV1LVGDiT:
         p = self.sd
         B, Lc, c_in = crossattn_emb.shape
         if cfg.use_crossattn_projection:
-            w, bias = p["crossattn_proj.0.weight"], p["crossattn_proj.0.bias"]
-            kp = (c_in + 1 + 63) // 64 * 64
-            if self.block_gemm == "own" and N.gemm_supported(w.shape[0], kp):
-                # crossattn_proj = Linear + bias + exact GELU (minimal_v4_dit.py:1430-1434, applied at :1604) on the
-                # hand-written GEMM: the bias rides as one more K column (a' = [emb | 1 | 0], w' = [w | bias | 0]), so
-                # it enters the fp32 accumulator before the product's one bf16 rounding, as the library's bias
-                # epilogue adds it; EPI_GELU then applies the GELU to the rounded sum (cp25_gelu's arithmetic).
-                if self._xproj_wb is None or self._xproj_wb.shape[1] != kp:
-                    wb = torch.zeros((w.shape[0], kp), dtype=BF16, device=self.device)
-                    wb[:, :c_in] = w
-                    wb[:, c_in] = bias
-                    self._xproj_wb = wb
-                a = torch.zeros((B * Lc, kp), dtype=BF16, device=self.device)
-                a[:, :c_in] = crossattn_emb.reshape(B * Lc, c_in)
-                a[:, c_in] = 1.0
-                ctx = N.gemm_epi(a, self._xproj_wb, epilogue=N.EPI_GELU)
-                del a
-            else:
-                ctx = F.linear(crossattn_emb.to(device=self.device, dtype=BF16), w, bias).reshape(B * Lc, -1).contiguous()
+            # crossattn_proj = Linear + bias + exact GELU (minimal_v4_dit.py:1430-1434, applied at :1604); EPI_GELU
+            # applies the GELU to the rounded sum (cp25_gelu's arithmetic)
+            ctx = self._bias_linear(crossattn_emb.reshape(B * Lc, c_in), "crossattn_proj.0", N.EPI_GELU)
+            if ctx is None:
+                ctx = F.linear(crossattn_emb.to(device=self.device, dtype=BF16), p["crossattn_proj.0.weight"],
+                               p["crossattn_proj.0.bias"]).reshape(B * Lc, -1).contiguous()
                 N.gelu_(ctx)
         else:
             ctx = crossattn_emb.to(device=self.device, dtype=BF16).reshape(B * Lc, c_in).contiguous()
@@ -544,6 +532,29 @@ class MinimalV1LVGDiT:
             ks.append(k.view(B, Lc, H, hd))
             vs.append(v.view(B, Lc, H, hd))
         return ContextCache(B=B, k=ks, v=vs)
+
+    def _bias_linear(self, x: torch.Tensor, key: str, epilogue: int = 0) -> Optional[torch.Tensor]:
+        """bf16 nn.Linear with bias (weight / bias `key`.weight / .bias) of x [M, K] on the hand-written GEMM: the bias
+        rides as one more K column (a' = [x | 1 | 0..], w' = [w | bias | 0..], K padded to a multiple of 64), so it
+        enters the fp32 accumulator before the product's one bf16 rounding, as the library's bias epilogue adds it
+        (tests/test_gemm_f32_gpu.py: bit-identical to F.linear(bias) on its case). None where the GEMM is not built
+        for the shape (the caller runs F.linear)."""
+        p = self.sd
+        w, bias = p[key + ".weight"], p[key + ".bias"]
+        n_out, k_in = w.shape
+        kp = (k_in + 1 + 63) // 64 * 64
+        if self.block_gemm != "own" or not N.gemm_supported(n_out, kp):
+            return None
+        wb = self._bias_w.get(key)
+        if wb is None:
+            wb = torch.zeros((n_out, kp), dtype=BF16, device=self.device)
+            wb[:, :k_in] = w
+            wb[:, k_in] = bias
+            self._bias_w[key] = wb
+        a = torch.zeros((x.shape[0], kp), dtype=BF16, device=self.device)
+        a[:, :k_in] = x
+        a[:, k_in] = 1.0
+        return N.gemm_epi(a, wb, epilogue=epilogue)
 
     def rope_tables(self, geo: Geometry) -> Tuple[torch.Tensor, torch.Tensor]:
         """cos/sin [n_tok, 64] of this shard; multi-view: every view's positions restart at t = 0
@@ -579,10 +590,16 @@ class MinimalV1LVGDiT:
                 raise ValueError(f"{A} actions, the net takes {cfg.num_action_per_chunk} per chunk")
             a = a.reshape(Ba, 1, A * dim)
 
-        def mlp(name):
-            h = F.linear(a, p[name + ".fc1.weight"], p[name + ".fc1.bias"])
+        def mlp(name):  # fc1 and fc2 (+ bias) on the hand-written GEMM, the tanh GELU between them in torch
+            x2 = a.reshape(-1, a.shape[-1])
+            h = self._bias_linear(x2, name + ".fc1")
+            if h is None:
+                h = F.linear(x2, p[name + ".fc1.weight"], p[name + ".fc1.bias"])
             h = F.gelu(h, approximate="tanh")
-            return F.linear(h, p[name + ".fc2.weight"], p[name + ".fc2.bias"])
+            y = self._bias_linear(h, name + ".fc2")
+            if y is None:
+                y = F.linear(h, p[name + ".fc2.weight"], p[name + ".fc2.bias"])
+            return y.view(*a.shape[:-1], -1)
 
         e_d, e_3d = mlp("action_embedder_B_D"), mlp("action_embedder_B_3D")
         if cfg.action_per_latent_frame:
@@ -677,12 +694,26 @@ class MinimalV1LVGDiT:
         if view_indices is None:
             view_indices = torch.arange(V, device=self.device)
         view_indices = view_indices.to(self.device).long().clamp(max=cfg.n_cameras_emb - 1)
-        emb = p["view_embeddings.weight"][view_indices].float()  # [V, vdim]
-        wv = w[:, f:].float().view(D, cfg.view_condition_dim, -1).sum(-1)  # [D, vdim]
-        bias = emb @ wv.t()  # [V, D]
+        vdim = cfg.view_condition_dim
+        if self._embed_f32 is None:
+            # fp32 weights zero-padded to K = 96 (patch features) and 32 (the view channels folded over (p1, p2, t))
+            w96 = torch.zeros((D, 96), dtype=F32, device=self.device)
+            w96[:, :f] = w[:, :f]
+            wv = torch.zeros((D, 32), dtype=F32, device=self.device)
+            wv[:, :vdim] = w[:, f:].float().view(D, vdim, -1).sum(-1)
+            self._embed_f32 = (w96, wv)
+        w96, wv = self._embed_f32
+        emb = torch.zeros((V, 32), dtype=F32, device=self.device)
+        emb[:, :vdim] = p["view_embeddings.weight"][view_indices]
+        bias = N.gemm_f32(emb, wv)  # [V, D]
         view_of_tok = torch.arange(geo.tok0, geo.tok0 + n, device=self.device) // geo.L_view
-        y = F.linear(patch_rows.reshape(n * Bx, f).float(), w[:, :f].float()).view(n, Bx, D)
-        return (y + bias[view_of_tok][:, None, :]).to(BF16)
+        rows = torch.zeros((n, Bx, 96), dtype=F32, device=self.device)
+        rows[:, :, :f] = patch_rows
+        # y[b] = rows[:, b] w96^T + bias[view of the token], batched over the Bx entries; fp32, rounded once
+        y = torch.empty((n, Bx, D), dtype=F32, device=self.device)
+        N.gemm_f32(rows.transpose(0, 1), w96.expand(Bx, D, 96), add=bias[view_of_tok].expand(Bx, n, D),
+                   out=y.transpose(0, 1), split_k=False)
+        return y.to(BF16)
 
     def forward_tokens(self, patch_rows: torch.Tensor, t_B_T: torch.Tensor, ctx: ContextCache,
                        geo: Geometry, action: Optional[torch.Tensor] = None,
