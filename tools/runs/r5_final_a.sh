@@ -4,7 +4,7 @@ set -o pipefail
 export PYTHONUNBUFFERED=1
 root=$(pwd)
 cd /tmp && export TMPDIR=/tmp && cd "$root"
-O=gpurun_out/r5fa
+O=gpurun_out/r5f${1:-a}
 mkdir -p $O
 timeout -k 10 700 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver_cmd.json 2> $O/bench_driver_cmd.err || { tail $O/bench_driver_cmd.err; exit 1; }
 python3 -c "
