@@ -74,6 +74,7 @@ SIGNATURES = {
     "cp25_ln_mod": [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _P, _P, _I64, _I, _I, _I64, _I64, _F, _P],
     "cp25_ln_mod_fp8": [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _P, _P, _P, _I64, _I, _I, _I64, _I64, _F, _P],
     "cp25_final_ln_mod": [_P, _P, _P, _I64, _I64, _P, _P, _I64, _I64, _P, _I64, _I, _I, _I64, _I64, _F, _P],
+    "cp25_layer_norm": [_P, _I64, _P, _P, _P, _I64, _I64, _I, _F, _P],
     "cp25_head_rmsnorm_rope": [_P, _I64, _I64, _I, _I, _I, _P, _P, _P, _P, _I64, _F, _P],
     "cp25_head_rmsnorm_rope_scaled": [_P, _I64, _I64, _I, _I, _I, _P, _P, _P, _P, _I64, _F, _F, _P],
     "cp25_head_rmsnorm_rope_nmax": [_P, _I64, _I64, _I, _I, _I, _P, _P, _P, _P, _I64, _F, _F, _P, _P],
@@ -462,6 +463,25 @@ def copy_rows(src: torch.Tensor, src_stride: int, dst: torch.Tensor, dst_stride:
     rc = lib.cp25_copy_rows(_ptr(src) + 2 * src_offset, src_stride, _ptr(dst), dst_stride, n_rows, width,
                             _stream(src.device))
     _check("cp25_copy_rows", rc)
+
+
+def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float = 1e-6,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Affine LayerNorm over the last dim of bf16 rows x [M, D] (row stride x.stride(0)) -> out [M, D] bf16
+    (cp25_layer_norm: fp32 statistics and affine, one rounding)."""
+    lib = load_library()
+    if x.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16 or bias.dtype != torch.bfloat16:
+        raise ValueError("layer_norm expects bf16 rows, weight and bias")
+    if x.dim() != 2 or x.stride(1) != 1 or not weight.is_contiguous() or not bias.is_contiguous():
+        raise ValueError("layer_norm: x [M, D] with contiguous rows, contiguous weight / bias")
+    M, D = x.shape
+    if weight.numel() != D or bias.numel() != D:
+        raise ValueError(f"layer_norm weight / bias must have {D} elements")
+    if out is None:
+        out = torch.empty((M, D), dtype=torch.bfloat16, device=x.device)
+    _check("cp25_layer_norm", lib.cp25_layer_norm(_ptr(x), x.stride(0), _ptr(weight), _ptr(bias), _ptr(out),
+                                                  out.stride(0), M, D, float(eps), _stream(x.device)))
+    return out
 
 
 def gelu_(x: torch.Tensor) -> torch.Tensor:

@@ -65,13 +65,24 @@ def state_dict_shapes(cfg: DiTConfig) -> Dict[str, Tuple[Tuple[int, ...], torch.
             s[p + a + ".output_proj.weight"] = ((D, D), BF16)
             s[p + a + ".q_norm.weight"] = ((hd,), BF16)
             s[p + a + ".k_norm.weight"] = ((hd,), BF16)
+        if cfg.cross_view_attn_map:  # MultiViewCrossBlock (multiview_cross_dit.py:282-290)
+            for m in ("q_proj", "k_proj", "v_proj", "output_proj"):
+                s[p + f"cross_view_attn.{m}.weight"] = ((D, D), BF16)
+            s[p + "cross_view_attn.q_norm.weight"] = ((hd,), BF16)
+            s[p + "cross_view_attn.k_norm.weight"] = ((hd,), BF16)
+            s[p + "layer_norm_cross_view_attn.weight"] = ((D,), BF16)
+            s[p + "layer_norm_cross_view_attn.bias"] = ((D,), BF16)
         s[p + "mlp.layer1.weight"] = ((cfg.mlp_hidden, D), BF16)
         s[p + "mlp.layer2.weight"] = ((D, cfg.mlp_hidden), BF16)
         for m in ("self_attn", "cross_attn", "mlp"):
             s[p + f"adaln_modulation_{m}.1.weight"] = ((A, D), BF16)
             s[p + f"adaln_modulation_{m}.2.weight"] = ((3 * D, A), BF16)
-    if cfg.n_cameras_emb:
+    if cfg.n_cameras_emb and cfg.view_condition_dim:
         s["view_embeddings.weight"] = ((cfg.n_cameras_emb, cfg.view_condition_dim), BF16)
+    if cfg.adaln_view_embedding:  # multiview_cross_dit.py:575-579
+        s["adaln_view_embedder.weight"] = ((cfg.n_cameras_emb, D), BF16)
+        s["adaln_view_proj.weight"] = ((9 * D, D), BF16)
+        s["adaln_view_proj.bias"] = ((9 * D,), BF16)
     if cfg.action_dim:
         fin, hid = cfg.action_in_features, cfg.action_hidden_features
         for name, out in (("action_embedder_B_D", D), ("action_embedder_B_3D", 3 * D)):
@@ -107,6 +118,16 @@ def init_state_dict(cfg: DiTConfig, seed: int = 0, device="cpu", zero_adaln_out:
             out[name] = (torch.arange(0, full, 2, device=device)[: shape[0]].float() / full).to(BF16)
         elif name == "view_embeddings.weight":  # multiview_dit.py:390-391
             out[name] = (torch.randn(shape, generator=g, device=device) * 0.02).to(BF16)
+        elif name == "adaln_view_embedder.weight":  # multiview_cross_dit.py:664-665
+            out[name] = (torch.randn(shape, generator=g, device=device) * 0.05).to(BF16)
+        elif name.startswith("adaln_view_proj") or name.endswith("cross_view_attn.output_proj.weight"):
+            # zero-initialised (:667-669, :306-309); zero_adaln_out=False fills them to exercise the path
+            out[name] = (torch.zeros(shape, dtype=BF16, device=device) if zero_adaln_out else
+                         tn(shape, 0.02 if name.endswith("bias") else 1.0 / math.sqrt(D)))
+        elif "layer_norm_cross_view_attn" in name:  # nn.LayerNorm init (1, 0); perturbed with zero_adaln_out=False
+            base = 1.0 if name.endswith("weight") else 0.0
+            noise = 0.0 if zero_adaln_out else 0.1
+            out[name] = (base + noise * torch.randn(shape, generator=g, device=device)).to(BF16)
         elif name.startswith("action_embedder"):  # nn.Linear default init (not covered by init_weights)
             fan_in = shapes_fan[name]
             bound = 1.0 / math.sqrt(fan_in)
@@ -449,6 +470,12 @@ class MinimalV1LVGDiT:
         self.w_t2 = p["t_embedder.1.linear_2.weight"].float()
         self.w_f1 = p["final_layer.adaln_modulation.1.weight"].float()
         self.w_f2 = p["final_layer.adaln_modulation.2.weight"].float()
+        if cfg.cross_view_attn_map:  # the cross-view q|k|v projections as one [3D, D] GEMM per block
+            self.w_cv_qkv = [torch.cat([p[f"blocks.{i}.cross_view_attn.{m}_proj.weight"] for m in "qkv"], 0).contiguous()
+                             for i in range(cfg.num_blocks)]
+        if cfg.adaln_view_embedding:
+            self.w_view_proj = p["adaln_view_proj.weight"].float()
+            self.b_view_proj = p["adaln_view_proj.bias"].float()
         self._bias_w = {}  # padded [w | bias | 0] copies for _bias_linear, per weight name
         self._embed_f32 = None  # multi-view patch embedding: fp32 weight padded to K = 96, view-channel fold
         self.refresh_norm_bounds()
@@ -471,6 +498,9 @@ class MinimalV1LVGDiT:
                             for i in range(cfg.num_blocks)]
         self.xattn_bounds = [(nb(p[f"blocks.{i}.cross_attn.q_norm.weight"]),
                               nb(p[f"blocks.{i}.cross_attn.k_norm.weight"])) for i in range(cfg.num_blocks)]
+        if cfg.cross_view_attn_map:
+            self.cvattn_bounds = [(nb(p[f"blocks.{i}.cross_view_attn.q_norm.weight"]),
+                                   nb(p[f"blocks.{i}.cross_view_attn.k_norm.weight"])) for i in range(cfg.num_blocks)]
 
     def attention_kernels(self, L: int) -> Dict[str, str]:
         """The attention kernel forms block 0 launches at L tokens (self) and against the text context (cross)."""
@@ -740,9 +770,21 @@ class MinimalV1LVGDiT:
         Bx = patch_rows.shape[1]
         x_in = self.embed_patches(patch_rows, geo, view_indices, rows_k128=rows_k128)
         mods, shift_f, scale_f = self.time_modulation(t_B_T, action)
+        if cfg.adaln_view_embedding:
+            mods = self._view_modulation(mods, geo, view_indices)
         cos, sin = self.rope_tables(geo)
         cp = self.cp_group
         cp_size = 1 if cp is None else torch.distributed.get_world_size(cp)
+        if cfg.cross_view_attn_map:
+            if cp_size > 1 or geo.n_tok != geo.L:
+                raise NotImplementedError("cross-view nets run without context parallelism (one shard = all tokens)")
+            cv = self._cross_view_neighbours(geo, view_indices)
+            gen = self._blocks(x_in, mods, shift_f, scale_f, ctx, geo, cos, sin, cp, cp_size, cv_nbrs=cv)
+            while True:
+                try:
+                    next(gen)
+                except StopIteration as e:
+                    return e.value
         if B == 1 or (cp_size == 1 and not self.force_lanes):
             gen = self._blocks(x_in, mods, shift_f, scale_f, ctx, geo, cos, sin, cp, cp_size, shared_batch)
             while True:
@@ -769,8 +811,89 @@ class MinimalV1LVGDiT:
                                       sin, cp, cp_size, prefix=prefix))
         return torch.cat(run_lanes(lanes), dim=1)
 
+    def _view_modulation(self, mods: torch.Tensor, geo: Geometry, view_indices: Optional[torch.Tensor]) -> torch.Tensor:
+        """Cross-view nets' AdaLN view embedding (multiview_cross_dit.py:807-813, 355-404): adaln_view_proj(
+        adaln_view_embedder(view id)) [V, 9D] (fp32, cp25_gemm_f32 with the bias as addend) in the chunk order
+        (shift, scale, gate) x (self-attn, cross-attn, mlp), rounded to bf16 and added to the bf16 modulation of every
+        frame of the view (one bf16 rounding, the reference's `m + view_m.type_as(x)`)."""
+        cfg, D, V = self.cfg, self.cfg.model_channels, geo.n_views
+        ids = self._view_ids(geo, view_indices)
+        e = self.sd["adaln_view_embedder.weight"][ids].float()
+        vp = N.gemm_f32(e, self.w_view_proj, add=self.b_view_proj).to(BF16).view(V, 3, 3 * D)
+        per_frame = vp.repeat_interleave(geo.T_view, dim=0)  # [T, 3, 3D]: frame t belongs to view t // T_view
+        if mods.shape[3] != per_frame.shape[0]:
+            raise ValueError(f"modulation has {mods.shape[3]} frames, the views {per_frame.shape[0]}")
+        return mods + per_frame.permute(1, 0, 2)[None, :, None]
+
+    def _view_ids(self, geo: Geometry, view_indices: Optional[torch.Tensor]) -> torch.Tensor:
+        V = geo.n_views
+        ids = torch.arange(V, device=self.device) if view_indices is None else view_indices.to(self.device).long()
+        if ids.numel() != V:
+            raise ValueError(f"{ids.numel()} view indices for {V} views")
+        return ids.clamp(max=self.cfg.n_cameras_emb - 1)
+
+    def _cross_view_neighbours(self, geo: Geometry, view_indices: Optional[torch.Tensor]) -> List[List[int]]:
+        """Per view position: the positions of its neighbour views present in the input, in the reference's key order
+        (CrossViewAttention.forward, multiview_cross_dit.py:160-186: neighbour ids of the view's id looked up among the
+        input's view ids, absent ones dropped -- the reference masks them -- positions sorted descending)."""
+        ids = self._view_ids(geo, view_indices).tolist()
+        amap = self.cfg.cross_view_attn_map
+        pos = {v: i for i, v in enumerate(ids)}
+        return [sorted((pos[u] for u in amap[v] if u in pos), reverse=True) if v < len(amap) else [] for v in ids]
+
+    def _per_view_attention(self, q, k, v, o, geo: Geometry, attn_kw: dict) -> None:
+        """Self-attention of each view over its own tokens ([B, n, H, hd] views, views contiguous along n): the
+        cross-view net's per-view self-attention (multiview_cross_dit.py:425-435, "(b v) (t h w)"). A q normalised in
+        the kernel reads the view's rows of the RoPE tables (positions restart per view)."""
+        if "fp8_qk" in attn_kw:
+            raise NotImplementedError("the fp8 attention forms are not built for per-view self-attention")
+        Lv = geo.L_view
+        for vi in range(geo.n_views):
+            sl = slice(vi * Lv, (vi + 1) * Lv)
+            kw = attn_kw
+            qn = attn_kw.get("q_norm")
+            if qn is not None and qn.get("cos") is not None:
+                kw = dict(attn_kw, q_norm=dict(qn, cos=qn["cos"][sl], sin=qn["sin"][sl]))
+            N.attn_fwd(q[:, sl], k[:, sl], v[:, sl], out=o[:, sl], **kw)
+
+    def _cross_view(self, i: int, x: torch.Tensor, B: int, geo: Geometry, nbrs: List[List[int]], mods_i1: torch.Tensor,
+                    lnk: dict, shift, scale):
+        """The cross-view sub-layer of MultiViewCrossBlock (multiview_cross_dit.py:436-450 over CrossViewAttention
+        :138-228): x + output_proj(attention of every view's tokens, per latent frame, to its neighbours' tokens of the
+        same frame) on the affine-LayerNormed x, un-gated; then the text cross-attention's LN-mod (shift, scale).
+        q / k / v come from one [3D, D] GEMM over all tokens (a neighbour's k / v rows are its own projections; the
+        reference projects the gathered neighbour rows, the same rows), q / k RMS-normed per head (no RoPE), and the
+        neighbours' K / V rows of each view gathered into one key sequence per frame. A view with no neighbour present
+        adds nothing (the reference would attend over an all-masked row). Returns (x', h)."""
+        cfg, p = self.cfg, self.sd
+        D, H, hd = cfg.model_channels, cfg.num_heads, cfg.head_dim
+        pre = f"blocks.{i}."
+        n, V, Tv, hw = geo.n_tok, geo.n_views, geo.T_view, geo.hw
+        hv = N.layer_norm(x.view(n * B, D), p[pre + "layer_norm_cross_view_attn.weight"],
+                          p[pre + "layer_norm_cross_view_attn.bias"])
+        w = self.w_cv_qkv[i]
+        qkv = N.gemm_epi(hv, w) if self._own(hv, w) else F.linear(hv, w)
+        q_scale, attn_kw = self._attn_mode(self.cvattn_bounds[i], hd)
+        N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=0, weight=p[pre + "cross_view_attn.q_norm.weight"],
+                            out_scale=q_scale)
+        N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=D, weight=p[pre + "cross_view_attn.k_norm.weight"])
+        q5 = qkv.view(V, Tv, hw, B, 3 * D)
+        o = torch.zeros((n, B, D), dtype=BF16, device=self.device)
+        o5 = o.view(V, Tv, hw, B, D)
+        for vi in range(V):
+            if not nbrs[vi]:
+                continue
+            # [Tv, n_nbr * hw, B, 2D]: frame t's key sequence = the neighbours' rows of frame t, in nbrs order
+            kv = torch.stack([q5[u, :, :, :, D:] for u in nbrs[vi]], dim=1).reshape(Tv, len(nbrs[vi]) * hw, B, 2 * D)
+            for b in range(B):
+                N.attn_fwd(q5[vi, :, :, b, :D].unflatten(-1, (H, hd)), kv[:, :, b, :D].unflatten(-1, (H, hd)),
+                           kv[:, :, b, D:].unflatten(-1, (H, hd)), out=o5[vi, :, :, b].unflatten(-1, (H, hd)), **attn_kw)
+        gate1 = torch.ones_like(mods_i1)[..., :D]  # the residual is not gated: bf16(1 * y) = y
+        return self._proj_res(o.view(n * B, D), p[pre + "cross_view_attn.output_proj.weight"],
+                              pre + "cross_view_attn.output_proj", x, B * D, D, gate1, B, geo, n, lnk, shift, scale)
+
     def _blocks(self, x_in, mods, shift_f, scale_f, ctx: ContextCache, geo: Geometry, cos, sin, cp, cp_size,
-                shared_batch: bool = False, prefix=None, prefix_only: bool = False):
+                shared_batch: bool = False, prefix=None, prefix_only: bool = False, cv_nbrs=None):
         """Generator: issues the 28 blocks + final layer for the batch entries in x_in/mods/ctx on the
         current stream; returns the final layer output [n, B, 64] fp32. Yields (so the caller can
         issue the other lane) right after each self-attention K/V gather is queued (CP > 1), or after
@@ -789,7 +912,8 @@ class MinimalV1LVGDiT:
         D, H, hd = cfg.model_channels, cfg.num_heads, cfg.head_dim
         n = geo.n_tok
         Bx = x_in.shape[1]
-        share0 = shared_batch and Bx == 1 and B > 1 and (cp is None or cp_size == 1) and self.share_cfg_block0
+        share0 = (shared_batch and Bx == 1 and B > 1 and (cp is None or cp_size == 1) and self.share_cfg_block0
+                  and cv_nbrs is None)
 
         def mod(i, j, nb=None):  # (shift, scale, gate) bf16 [B, T, D] views of block i, sub-layer j (first nb)
             m = mods[i, j] if nb is None else mods[i, j][:nb]
@@ -838,8 +962,11 @@ class MinimalV1LVGDiT:
                     attn_kw = self._fp8_qk(qkv[:, :D], qkv[:, D:2 * D], Bs, H, hd, attn_kw, vv)
                     if ev is not None:
                         ev[0].record()
-                    N.attn_fwd(q, kk, vv, out=o.view(n, Bs, H, hd).transpose(0, 1), **attn_kw)
-                    lk = kk.shape[1]
+                    if cv_nbrs is not None:
+                        self._per_view_attention(q, kk, vv, o.view(n, Bs, H, hd).transpose(0, 1), geo, attn_kw)
+                    else:
+                        N.attn_fwd(q, kk, vv, out=o.view(n, Bs, H, hd).transpose(0, 1), **attn_kw)
+                    lk = kk.shape[1] if cv_nbrs is None else geo.L_view
                 else:
                     yield from self._cp_self_attention(i, h, o, cos, sin, n, B, cp, cp_size,
                                                        ev[0] if ev is not None else None)
@@ -855,8 +982,17 @@ class MinimalV1LVGDiT:
                     x_st, x_sb = x_in.stride(0), (0 if Bx == 1 else x_in.stride(1))
                 else:
                     x_st, x_sb = B * D, D
-                x, h = self._proj_res(o.view(n * Bs, D), p[pre + "self_attn.output_proj.weight"], pre + "self_attn.output_proj",
-                                      x, x_st, x_sb, g_sa, Bs, geo, n, lnk, sh, sc)
+                wo = p[pre + "self_attn.output_proj.weight"]
+                if cv_nbrs is not None:
+                    # the cross-view sub-layer sits between the self-attention residual and the text cross-attention's
+                    # LN-mod (the library path computes that LN-mod here too and drops it)
+                    fused = self._fused_res(o.view(n * Bs, D), wo, Bs, geo.hw)
+                    x, _ = self._proj_res(o.view(n * Bs, D), wo, pre + "self_attn.output_proj", x, x_st, x_sb, g_sa, Bs,
+                                          geo, n, lnk, None if fused else sh, None if fused else sc)
+                    x, h = self._cross_view(i, x, B, geo, cv_nbrs, mods[i, 1], lnk, sh, sc)
+                else:
+                    x, h = self._proj_res(o.view(n * Bs, D), wo, pre + "self_attn.output_proj", x, x_st, x_sb, g_sa, Bs,
+                                          geo, n, lnk, sh, sc)
             if prefix_only:
                 return x, h
             # ---- cross attention (a shared query is read with batch stride 0 against each entry's text K/V)

@@ -57,6 +57,14 @@ class DiTConfig:
     n_cameras_emb: int = 0
     view_condition_dim: int = 0
     state_t: int = 0
+    # cross-view multi-view net (MultiViewCrossDiT, predict2_multiview/networks/multiview_cross_dit.py:502-869):
+    # adaln_view_embedding adds adaln_view_embedder (nn.Embedding(n_cameras_emb, D)) + adaln_view_proj (Linear(D, 9D))
+    # whose 9 chunks are added to every block's shift / scale / gate per view (:355-404); a non-empty
+    # cross_view_attn_map (neighbour view ids per view id) enables per-view self-attention plus a CrossViewAttention
+    # sub-layer after it (:115-228, 436-450): per latent frame, each view's tokens attend to its neighbours' tokens of
+    # the same frame, un-gated residual after an affine LayerNorm
+    adaln_view_embedding: bool = False
+    cross_view_attn_map: tuple = ()
 
     @property
     def head_dim(self) -> int:
@@ -119,6 +127,17 @@ SAMPLER_ACTION = SamplerConfig(state_t=4, resolution="256")
 DIT_2B_MULTIVIEW = DIT_2B.replace(n_cameras_emb=7, view_condition_dim=7, state_t=8,
                                   rope_t_extrapolation_ratio=8.0 / 24.0)
 SAMPLER_MULTIVIEW = SamplerConfig(state_t=8, cfg_mode="text2world", resolution="720")
+# cross-view multi-view net (COSMOS_V1_2B_MULTIVIEW_CROSSVIEW_NET, predict2_multiview/configs/vid2vid/defaults/net.py:
+# 76-107: adaln view embedding, no view-embedding input channels, cross-view attention) with the crossview experiment's
+# neighbour map (experiment/buttercup/buttercup2p5_rectified_flow.py:387-399) in the view ids of
+# predict2_multiview/scripts/inference.py:61-69 (front_wide 0, cross_right 1, rear_right 2, rear_tele 3, rear_left 4,
+# cross_left 5, front_tele 6); state_t and RoPE as the multiview experiment above. The registered config sets
+# use_wan_fp32_strategy=False, whose conditioning precision is the caller's autocast; this build runs the conditioning
+# in fp32 (the fp32 strategy) for every net.
+CROSS_VIEW_MAP_7 = ((5, 1, 6), (0, 2), (1, 3), (4, 2), (5, 3), (0, 4), (0,))
+DIT_2B_MULTIVIEW_CROSSVIEW = DIT_2B.replace(n_cameras_emb=7, view_condition_dim=0, state_t=8,
+                                            rope_t_extrapolation_ratio=8.0 / 24.0, adaln_view_embedding=True,
+                                            cross_view_attn_map=CROSS_VIEW_MAP_7)
 
 # model name (cosmos_predict2/config.py ModelKey.name) -> (net, sampler)
 MODELS = {
@@ -127,6 +146,8 @@ MODELS = {
     "14B/pre-trained": (DIT_14B, SAMPLER_PRE_TRAINED),
     "2B/robot/action-cond": (DIT_2B_ACTION, SAMPLER_ACTION),
     "2B/auto/multiview": (DIT_2B_MULTIVIEW, SAMPLER_MULTIVIEW),
+    # the reference registers this net (hydra net "cosmos_v1_2B_multiview_crossview") but ships no checkpoint for it
+    "2B/auto/multiview-crossview": (DIT_2B_MULTIVIEW_CROSSVIEW, SAMPLER_MULTIVIEW),
 }
 
 # Subset of VIDEO_RES_SIZE_INFO (cosmos_predict2/_src/predict2/datasets/utils.py:44-67); the model's

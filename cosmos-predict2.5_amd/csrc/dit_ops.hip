@@ -6,6 +6,8 @@
 //                          minimal_v4_dit.py:1171-1179 (_fn), :1204 / :1237 / :1246 (gated residuals)
 //   cp25_final_ln_mod    : fp32-autocast variant for the final layer                         (fp32 out)
 //                          minimal_v4_dit.py:974-991
+//   cp25_layer_norm      : affine LayerNorm (the cross-view net's layer_norm_cross_view_attn)    (bf16)
+//                          predict2_multiview/networks/multiview_cross_dit.py:290, :441
 //   cp25_head_rmsnorm_rope: per-head RMSNorm (TE, eps 1e-6) of q and k, optional 3D RoPE in fp32,
 //                          result rounded to bf16 as attention() does (minimal_v4_dit.py:410-420,
 //                          attention.py:107-109)
@@ -127,6 +129,55 @@ __global__ void __launch_bounds__(256) ln_mod_kernel(
       }
       *reinterpret_cast<u32x2*>(h8_out + row * D + (c * 64 + lane) * 8) = o8;
     }
+  }
+}
+
+// ---------------------------------------------------------------- affine LayerNorm (no modulation)
+// nn.LayerNorm(D, elementwise_affine=True, eps) on bf16 rows: fp32 mean / variance (two passes over the registers, as
+// ln_mod_kernel), y = (x - mean) * rstd * w + b in fp32, one bf16 rounding (torch's layer_norm on bf16 input and
+// weights). One wave per row. The cross-view net's layer_norm_cross_view_attn (multiview_cross_dit.py:290, :441).
+template <int NC>
+__global__ void __launch_bounds__(256) layer_norm_kernel(const unsigned short* __restrict__ x, int64_t x_stride,
+                                                         const unsigned short* __restrict__ w,
+                                                         const unsigned short* __restrict__ bias,
+                                                         unsigned short* __restrict__ y, int64_t y_stride,
+                                                         int64_t n_rows, float eps) {
+  constexpr int D = NC * 512;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n_rows) return;
+  float v[NC * 8];
+  const unsigned short* xr = x + row * x_stride;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    u16x8 t = *reinterpret_cast<const u16x8*>(xr + (c * 64 + lane) * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[c * 8 + e] = bf2f(t[e]);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NC * 8; ++i) s += v[i];
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+  const float mean = s * (1.f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NC * 8; ++i) {
+    const float d = v[i] - mean;
+    q += d * d;
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) q += __shfl_xor(q, m);
+  const float rstd = rsqrtf(q * (1.f / D) + eps);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int off = (c * 64 + lane) * 8;
+    u16x8 wv = *reinterpret_cast<const u16x8*>(w + off);
+    u16x8 bv = *reinterpret_cast<const u16x8*>(bias + off);
+    u16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf((v[c * 8 + e] - mean) * rstd * bf2f(wv[e]) + bf2f(bv[e]));
+    *reinterpret_cast<u16x8*>(y + row * y_stride + off) = o;
   }
 }
 
@@ -428,6 +479,30 @@ extern "C" int cp25_final_ln_mod(const void* x, const void* y, const void* gate,
     default: return CP25_ERR_DTYPE;
   }
 #undef FLN
+  CP25_LAUNCH_CHECK();
+  return CP25_OK;
+}
+
+extern "C" int cp25_layer_norm(const void* x, int64_t x_stride, const void* weight, const void* bias, void* y,
+                               int64_t y_stride, int64_t n_rows, int D, float eps, hipStream_t stream) {
+  if (!x || !weight || !bias || !y || n_rows <= 0 || x_stride < D || y_stride < D) return CP25_ERR_INVAL;
+  if ((x_stride % 8) || (y_stride % 8) || (((uintptr_t)x | (uintptr_t)y | (uintptr_t)weight | (uintptr_t)bias) & 15))
+    return CP25_ERR_INVAL;
+  const dim3 grid((unsigned)cdiv(n_rows, 4));
+  auto* X = (const unsigned short*)x;
+  auto* W = (const unsigned short*)weight;
+  auto* Bi = (const unsigned short*)bias;
+  auto* Y = (unsigned short*)y;
+#define LNA(NC) hipLaunchKernelGGL(layer_norm_kernel<NC>, grid, dim3(256), 0, stream, X, x_stride, W, Bi, Y, y_stride, n_rows, eps)
+  switch (D) {
+    case 512: LNA(1); break;
+    case 1024: LNA(2); break;
+    case 2048: LNA(4); break;
+    case 4096: LNA(8); break;
+    case 5120: LNA(10); break;
+    default: return CP25_ERR_DTYPE;
+  }
+#undef LNA
   CP25_LAUNCH_CHECK();
   return CP25_OK;
 }

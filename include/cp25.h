@@ -199,6 +199,14 @@ int cp25_final_ln_mod(const void* x, const void* y, const void* gate, int64_t gm
                       const float* shift, const float* scale, int64_t mod_sb, int64_t mod_st, float* out,
                       int64_t n_tok, int B, int D, int64_t tok0, int64_t hw, float eps, hipStream_t stream);
 
+/* Affine LayerNorm of n_rows bf16 rows (row stride x_stride / y_stride elements, multiples of 8; 16-B aligned
+ * pointers): y = (x - mean) * rstd * weight + bias in fp32 with fp32 statistics, one bf16 rounding (nn.LayerNorm with
+ * elementwise_affine on bf16). D in {512, 1024, 2048, 4096, 5120}.
+ * Replaces: MultiViewCrossBlock.layer_norm_cross_view_attn, predict2_multiview/networks/multiview_cross_dit.py:290,
+ * :441. */
+int cp25_layer_norm(const void* x, int64_t x_stride, const void* weight, const void* bias, void* y, int64_t y_stride,
+                    int64_t n_rows, int D, float eps, hipStream_t stream);
+
 /* In-place per-head RMSNorm (weight[128] bf16, eps) of heads [head_off, head_off + H*128) of every
  * row of a bf16 [n_rows, row_stride] buffer, then (if cos_tab != NULL) rotate-half RoPE in fp32
  * with cos/sin tables [n_tok, 64] fp32 indexed by token = row / B, result rounded to bf16.

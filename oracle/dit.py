@@ -222,20 +222,57 @@ def ln_mod(x, shift, scale):
     return F.layer_norm(x, (x.shape[-1],), eps=1e-6) * (1 + scale) + shift
 
 
-def block_forward(cfg, sd, i, x, emb, lora, ctx, freqs, n_views: int = 1):
-    """Block.forward, x [B, T, H, W, D] bf16 (multi-view: MultiViewBlock, per-view cross-attention)."""
+def cross_view_attention(cfg, sd, p, x, n_views: int, view_ids) -> torch.Tensor:
+    """MultiViewCrossBlock's cross-view sub-layer (predict2_multiview/networks/multiview_cross_dit.py:436-450) over
+    CrossViewAttention.forward (:138-228), x [B, T, H, W, D] with the views stacked along T: the affine LayerNorm, then
+    per (batch entry, latent frame, view) the view's H*W tokens attend to its neighbours' tokens of the same frame
+    (neighbour ids of the view's id from the map, looked up among the input's view ids; absent ones masked, i.e.
+    left out; key order: neighbour positions sorted descending, :177-186), q / k RMS-normed, no RoPE; output_proj;
+    the un-gated residual. A view with no neighbour present contributes nothing (the reference's all-masked row)."""
+    nh, hd = cfg["num_heads"], cfg["model_channels"] // cfg["num_heads"]
+    B, T, H, W, D = x.shape
+    Tv, hw = T // n_views, H * W
+    xn = F.layer_norm(x, (D,), _w(sd, p + "layer_norm_cross_view_attn.weight"),
+                      _w(sd, p + "layer_norm_cross_view_attn.bias"), eps=1e-6)
+    xv = xn.reshape(B, n_views, Tv, hw, D)
+    q = te_rmsnorm(_lin(xv, _w(sd, p + "cross_view_attn.q_proj.weight")).reshape(B, n_views, Tv, hw, nh, hd),
+                   _w(sd, p + "cross_view_attn.q_norm.weight"))
+    k = te_rmsnorm(_lin(xv, _w(sd, p + "cross_view_attn.k_proj.weight")).reshape(B, n_views, Tv, hw, nh, hd),
+                   _w(sd, p + "cross_view_attn.k_norm.weight"))
+    v = _lin(xv, _w(sd, p + "cross_view_attn.v_proj.weight")).reshape(B, n_views, Tv, hw, nh, hd)
+    amap = cfg["cross_view_attn_map"]
+    pos = {int(vid): j for j, vid in enumerate(view_ids)}
+    o = torch.zeros(B, n_views, Tv, hw, nh * hd, dtype=act_dtype(), device=x.device)
+    for j, vid in enumerate(view_ids):
+        nb = sorted((pos[u] for u in amap[int(vid)] if u in pos), reverse=True) if int(vid) < len(amap) else []
+        if not nb:
+            continue
+        kk = torch.cat([k[:, u] for u in nb], dim=2)  # [B, Tv, n_nb * hw, nh, hd]
+        vv = torch.cat([v[:, u] for u in nb], dim=2)
+        oj = sdpa(q[:, j].reshape(B * Tv, hw, nh, hd), kk.reshape(B * Tv, -1, nh, hd), vv.reshape(B * Tv, -1, nh, hd))
+        o[:, j] = oj.reshape(B, Tv, hw, nh * hd)
+    out = _lin(o, _w(sd, p + "cross_view_attn.output_proj.weight")).reshape(B, T, H, W, D)
+    return x + out
+
+
+def block_forward(cfg, sd, i, x, emb, lora, ctx, freqs, n_views: int = 1, view_mod=None, view_ids=None):
+    """Block.forward, x [B, T, H, W, D] bf16 (multi-view: MultiViewBlock, per-view cross-attention; cross-view nets:
+    MultiViewCrossBlock, multiview_cross_dit.py:313-500 -- per-view self-attention, the cross-view sub-layer, and the
+    view modulation view_mod [9, T, D] bf16 added to the bf16 shift / scale / gate, :355-404)."""
     p = f"blocks.{i}."
     nh, hd = cfg["num_heads"], cfg["model_channels"] // cfg["num_heads"]
     sh_sa, sc_sa, g_sa = adaln(sd, p + "adaln_modulation_self_attn", emb, lora)
     sh_ca, sc_ca, g_ca = adaln(sd, p + "adaln_modulation_cross_attn", emb, lora)
     sh_ml, sc_ml, g_ml = adaln(sd, p + "adaln_modulation_mlp", emb, lora)
     cvt = lambda t: t[:, :, None, None, :].to(act_dtype())  # noqa: E731
-    sh_sa, sc_sa, g_sa, sh_ca, sc_ca, g_ca, sh_ml, sc_ml, g_ml = map(
-        cvt, (sh_sa, sc_sa, g_sa, sh_ca, sc_ca, g_ca, sh_ml, sc_ml, g_ml)
-    )
+    mods = [cvt(t) for t in (sh_sa, sc_sa, g_sa, sh_ca, sc_ca, g_ca, sh_ml, sc_ml, g_ml)]
+    if view_mod is not None:
+        mods = [m + view_mod[j][None, :, None, None, :].to(act_dtype()) for j, m in enumerate(mods)]
+    sh_sa, sc_sa, g_sa, sh_ca, sc_ca, g_ca, sh_ml, sc_ml, g_ml = mods
     B, T, H, W, D = x.shape
+    cross_view = bool(cfg.get("cross_view_attn_map"))
 
-    # self attention
+    # self attention (cross-view nets: per view, "(b v) (t h w)")
     h = ln_mod(x, sh_sa, sc_sa).reshape(B, T * H * W, D)
     q = _lin(h, _w(sd, p + "self_attn.q_proj.weight")).reshape(B, -1, nh, hd)
     k = _lin(h, _w(sd, p + "self_attn.k_proj.weight")).reshape(B, -1, nh, hd)
@@ -244,9 +281,15 @@ def block_forward(cfg, sd, i, x, emb, lora, ctx, freqs, n_views: int = 1):
     k = te_rmsnorm(k, _w(sd, p + "self_attn.k_norm.weight")).float()
     q = apply_rope(q, freqs)
     k = apply_rope(k, freqs)
-    o = sdpa(q.to(act_dtype()), k.to(act_dtype()), v.to(act_dtype()))
+    if cross_view:
+        sv = lambda t: t.to(act_dtype()).reshape(B * n_views, -1, nh, hd)  # noqa: E731
+        o = sdpa(sv(q), sv(k), sv(v)).reshape(B, T * H * W, nh * hd)
+    else:
+        o = sdpa(q.to(act_dtype()), k.to(act_dtype()), v.to(act_dtype()))
     o = _lin(o, _w(sd, p + "self_attn.output_proj.weight")).reshape(B, T, H, W, D)
     x = x + g_sa * o
+    if cross_view:
+        x = cross_view_attention(cfg, sd, p, x, n_views, view_ids)
 
     # cross attention (no RoPE)
     h = ln_mod(x, sh_ca, sc_ca).reshape(B, T * H * W, D)
@@ -277,7 +320,8 @@ def block_forward(cfg, sd, i, x, emb, lora, ctx, freqs, n_views: int = 1):
 
 def dit_forward(cfg: dict, sd: dict, x_B_C_T_H_W: torch.Tensor, timesteps_B_T: torch.Tensor,
                 crossattn_emb: torch.Tensor, cond_mask_B_1_T_H_W: torch.Tensor,
-                padding_mask_B_1_H_W: torch.Tensor | None = None, action: torch.Tensor | None = None) -> torch.Tensor:
+                padding_mask_B_1_H_W: torch.Tensor | None = None, action: torch.Tensor | None = None,
+                view_ids=None) -> torch.Tensor:
     """-> velocity [B, C, T, H, W] fp32 (the model applies .float(), text2world_model_rectified_flow.py:860)."""
     x = x_B_C_T_H_W.to(act_dtype())
     B, C, T, Hl, Wl = x.shape
@@ -288,9 +332,12 @@ def dit_forward(cfg: dict, sd: dict, x_B_C_T_H_W: torch.Tensor, timesteps_B_T: t
         pm = F.interpolate(pm.float(), size=(Hl, Wl), mode="nearest").to(act_dtype())
         x = torch.cat([x, pm[:, :, None].expand(B, 1, T, Hl, Wl)], dim=1)
     n_views = T // cfg["state_t"] if cfg.get("n_cameras_emb", 0) else 1
-    if n_views > 1 or cfg.get("n_cameras_emb", 0):
+    if view_ids is None:
+        view_ids = list(range(n_views))
+    view_ids = [min(int(v), cfg.get("n_cameras_emb", 1) - 1) for v in view_ids]
+    if cfg.get("view_condition_dim", 0):
         # concat_view_embedding (multiview_dit.py:462-490): view channels after [x, mask, padding mask]
-        vidx = torch.arange(n_views, device=x.device).clamp(max=cfg["n_cameras_emb"] - 1)
+        vidx = torch.tensor(view_ids, device=x.device)
         ve = _w(sd, "view_embeddings.weight")[vidx]  # [V, vdim] bf16
         Tv = T // n_views
         vch = ve.t()[None, :, :, None, None, None].expand(B, ve.shape[1], n_views, Tv, Hl, Wl)
@@ -309,8 +356,15 @@ def dit_forward(cfg: dict, sd: dict, x_B_C_T_H_W: torch.Tensor, timesteps_B_T: t
         ctx = F.gelu(_lin(ctx, _w(sd, "crossattn_proj.0.weight"), _w(sd, "crossattn_proj.0.bias")))
 
     emb, lora = timestep_embedding(cfg, sd, t, action)
+    view_mod = None
+    if cfg.get("adaln_view_embedding"):
+        # adaln_view_proj(adaln_view_embedder(view id)) (multiview_cross_dit.py:807-813; fp32 as the conditioning
+        # strategy of this build) -> 9 chunks, each per frame of its view, cast to the activation dtype
+        e = _w(sd, "adaln_view_embedder.weight")[torch.tensor(view_ids, device=x.device)].float()
+        vp = _lin(e, _w(sd, "adaln_view_proj.weight").float(), _w(sd, "adaln_view_proj.bias").float())
+        view_mod = vp.to(act_dtype()).view(n_views, 9, -1).repeat_interleave(Tp // n_views, dim=0).transpose(0, 1)
     for i in range(cfg["num_blocks"]):
-        x = block_forward(cfg, sd, i, x, emb, lora, ctx, freqs, n_views)
+        x = block_forward(cfg, sd, i, x, emb, lora, ctx, freqs, n_views, view_mod, view_ids)
 
     # final layer (fp32 autocast)
     D = cfg["model_channels"]

@@ -129,6 +129,14 @@ def gemm_res(a, w, x, x_st, x_sb, gate, *, B, tok0, hw, out=None):
     return out
 
 
+def layer_norm(x, weight, bias, eps=1e-6, out=None):
+    y = F.layer_norm(x.float(), (x.shape[-1],), weight.float(), bias.float(), eps=eps).to(BF16)
+    if out is None:
+        return y
+    out.copy_(y)
+    return out
+
+
 def gelu_(x):
     x.copy_(F.gelu(x))
     return x
@@ -201,7 +209,7 @@ def vae_attn(q, k, v, out=None, scale=None):
 
 _FUNCS = dict(conv3d=conv3d, rms_norm_silu=rms_norm_silu, vae_attn=vae_attn, ln_mod=ln_mod, final_ln_mod=final_ln_mod, head_rmsnorm_rope=head_rmsnorm_rope, copy_rows=copy_rows,
               attn_fwd=attn_fwd, attn_kernel_name=attn_kernel_name, gemm_epi=gemm_epi, gemm_f32=gemm_f32, gemm_res=gemm_res,
-              gemm_hnorm=gemm_hnorm, gemm_qkv=gemm_qkv, gelu_=gelu_)
+              gemm_hnorm=gemm_hnorm, gemm_qkv=gemm_qkv, gelu_=gelu_, layer_norm=layer_norm)
 
 
 @contextlib.contextmanager
