@@ -5,9 +5,10 @@ export PYTHONUNBUFFERED=1
 O=gpurun_out/r5simcp
 mkdir -p $O
 timeout -k 10 900 python tools/sim_cp_rank.py --cp 1 2 4 8 --iters 2 > $O/sim2b.log 2> $O/sim2b.err || { tail -20 $O/sim2b.err; exit 1; }
-grep '^{' $O/sim2b.log | python3 -c "
+for f in sim2b; do echo $f; grep "^{" $O/$f.log | python3 -c "
 import json, sys
 rows = [json.loads(l) for l in sys.stdin]
 base = [r for r in rows if r['cp'] == 1][0]['forward_s']
 for r in rows:
     print(r['cp'], round(r['forward_s'], 4), 'eff', round(base / r['cp'] / r['forward_s'], 4))"
+done
