@@ -709,16 +709,21 @@ class MinimalV1LVGDiT:
         if not cfg.view_condition_dim:
             if rows_k128 and (Bx != 1 or f != 72 or patch_rows.stride(0) != 128 or patch_rows.stride(2) != 1):
                 raise ValueError("rows_k128: expected the [n, 1, 72] view of patchify(ld=128)'s [n, 128] buffer")
-            if rows_k128 and self.block_gemm == "own" and N.gemm_supported(D, 128):
-                # rows from patchify(ld=128): the zero-padded K = 128 operand of the own GEMM against the weight
-                # zero-padded to 128 columns (the same sums as K = 72; the library GEMM took K = 72 before)
-                a = torch.as_strided(patch_rows, (n, 128), (128, 1))
+            if self.block_gemm == "own" and N.gemm_supported(D, 128) and f <= 128:
+                # the zero-padded K = 128 operand of the own GEMM against the weight zero-padded to 128 columns (the
+                # same sums as K = 72): rows from patchify(ld=128) are that operand already, other rows are copied
+                # into it
+                if rows_k128:
+                    a = torch.as_strided(patch_rows, (n, 128), (128, 1))
+                else:
+                    a = torch.zeros((n * Bx, 128), dtype=BF16, device=self.device)
+                    a[:, :f] = patch_rows.reshape(n * Bx, f)
                 wp = self._x_embed_w128
                 if wp is None or wp.shape[0] != D:
                     wp = torch.zeros((D, 128), dtype=BF16, device=self.device)
                     wp[:, :f] = w[:, :f]
                     self._x_embed_w128 = wp
-                return N.gemm_epi(a, wp).view(n, 1, D)
+                return N.gemm_epi(a, wp).view(n, Bx, D)
             return F.linear(patch_rows.reshape(n * Bx, f), w).view(n, Bx, D)
         V = geo.n_views
         if view_indices is None:

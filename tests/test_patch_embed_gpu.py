@@ -43,5 +43,10 @@ def test_embed_patches_own_gemm(device):
     diff = (own.float() - lib.float()).abs()
     ulp = lib.float().abs().clamp_min(1e-3) * 2.0 ** -7
     assert (diff <= ulp).all(), diff.max().item()
-    # without the flag the same strided view takes the library GEMM over its 72 columns (never the padded storage)
-    assert torch.equal(net.embed_patches(rows.view(n, 1, 72), geo), lib)
+    # without the flag the 72 columns are copied into a zero-padded operand (never read from the padded storage): the
+    # same operand, the same GEMM, the same bits; likewise per batch entry for [n, 2, 72] rows
+    assert torch.equal(net.embed_patches(rows.view(n, 1, 72), geo), own)
+    rows2 = torch.stack([rows, rows.flip(0)], 1).contiguous()
+    two = net.embed_patches(rows2, geo)
+    assert two.shape == (n, 2, own.shape[-1])
+    assert torch.equal(two[:, :1], own) and torch.equal(two[:, 1:], net.embed_patches(rows.flip(0).view(n, 1, 72), geo))
