@@ -194,3 +194,34 @@ def test_full_depth_2b_sampler(device, net2b, guidance):
     assert d["hip_truth"] <= 1.05 * d["ref_truth"], d
     if guidance > 0:
         assert d["hip_ref"] <= 0.95 * d["ref_truth"], d
+
+
+def test_full_depth_crossview_forward(device):
+    """The 28-block 2B cross-view net (DIT_2B_MULTIVIEW_CROSSVIEW, multiview_cross_dit.py) against the fp32 truth:
+    3 rig views (ids 0, 1, 5: front_wide with two of its three neighbours present, cross_right and cross_left with
+    front_wide), 2 latent frames per view of 8 x 8 tokens, the same gate as the single-view forward."""
+    from cosmos_predict2.net_config import DIT_2B_MULTIVIEW_CROSSVIEW
+
+    cfg = DIT_2B_MULTIVIEW_CROSSVIEW.replace(state_t=2)
+    sd = {"net." + k: v for k, v in init_state_dict(cfg, seed=13, zero_adaln_out=False).items()}
+    view_ids = [0, 1, 5]
+    g = torch.Generator().manual_seed(37)
+    T, H, W = 6, 16, 16
+    x = torch.randn(1, 16, T, H, W, generator=g)
+    mask = torch.zeros(1, 1, T, H, W)
+    mask[:, :, ::2] = 1
+    t = torch.tensor([[0.1, 877.0] * 3])
+    ctx = torch.randn(1, 512 * 3, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
+    c = dataclasses.asdict(cfg)
+    ref = odit.dit_forward(c, sd, x, t, ctx, mask, view_ids=view_ids)
+    with odit.fp32_truth():
+        truth = odit.dit_forward(c, sd, x, t, ctx, mask, view_ids=view_ids)
+    net = MinimalV1LVGDiT(cfg, device=device)
+    net.load_state_dict(sd)
+    vi = torch.tensor([view_ids]).repeat_interleave(2, dim=1)
+    hip = net(x.to(device).to(torch.bfloat16), t.to(device), ctx.to(device),
+              condition_video_input_mask_B_C_T_H_W=mask.to(device), view_indices_B_T=vi.to(device)).cpu()
+    d = _report("28-block 2B cross-view forward (3 views)", hip, ref, truth)
+    assert torch.isfinite(hip).all()
+    assert d["hip_truth"] <= 1.1 * d["ref_truth"], d
+    assert d["hip_ref"] <= 1.2e-2, d
