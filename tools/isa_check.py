@@ -14,7 +14,19 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def compile_asm(src, out="/tmp/isa_check.s", extra=()):
+_ASM_CACHE = {}
+
+
+def compile_asm(src, out=None, extra=()):
+    """(asm text, resource remarks per kernel) of src; cached per (source path, mtime, extra flags) in this process,
+    so several checks of one source compile it once."""
+    key = (os.path.abspath(src), os.path.getmtime(src), tuple(extra))
+    if key not in _ASM_CACHE:
+        _ASM_CACHE[key] = _compile_asm(src, out or f"/tmp/isa_check_{os.getpid()}_{os.path.basename(src)}.s", extra)
+    return _ASM_CACHE[key]
+
+
+def _compile_asm(src, out, extra=()):
     unit_flags = ["-fno-honor-nans", "-fno-slp-vectorize"] if os.path.basename(src).startswith(("attn_fwd", "vae_attn")) \
         else []  # the Makefile's per-unit flags
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
