@@ -1070,6 +1070,11 @@ class MinimalV1LVGDiT:
             ks = slice(vi * 512, (vi + 1) * 512)
             N.attn_fwd(q[a:b].transpose(0, 1), k[:, ks], v[:, ks], out=o[a:b].transpose(0, 1), **attn_kw)
 
+    def _kv_gather_buffer(self, shape) -> torch.Tensor:
+        """The all-gather's destination for one lane-block's K|V rows (a fresh caching-allocator buffer; the one-GPU
+        rank simulation, tools/sim_cp_rank.py --gather none, substitutes a persistent pre-filled one)."""
+        return torch.empty(shape, dtype=BF16, device=self.device)
+
     def _cp_self_attention(self, i: int, h: torch.Tensor, o: torch.Tensor, cos, sin, n: int, B: int, cp,
                            cp_size: int, e0=None):
         """Self-attention of a context-parallel token shard (replaces the reference's Ulysses
@@ -1083,7 +1088,7 @@ class MinimalV1LVGDiT:
         qkv = self._qkv_k_normed(h, i, n * B, B, cos, sin)  # [n*B, 3D], k normed + roped
         kv = torch.empty((n * B, 2 * D), dtype=BF16, device=self.device)
         N.copy_rows(qkv, 3 * D, kv, 2 * D, n * B, 2 * D, src_offset=D)
-        kv_all = torch.empty((cp_size * n * B, 2 * D), dtype=BF16, device=self.device)
+        kv_all = self._kv_gather_buffer((cp_size * n * B, 2 * D))
         work = all_gather_into_async(kv_all, kv, cp)  # RCCL over xGMI
         yield i  # the other lane's block runs here (in issue order) while this gather is in flight
         q_scale, attn_kw = self._self_attn_mode(i, hd)
