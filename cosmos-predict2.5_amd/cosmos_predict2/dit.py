@@ -1086,6 +1086,8 @@ class MinimalV1LVGDiT:
         pre = f"blocks.{i}."
         D, H, hd = cfg.model_channels, cfg.num_heads, cfg.head_dim
         qkv = self._qkv_k_normed(h, i, n * B, B, cos, sin)  # [n*B, 3D], k normed + roped
+        # (q and k|v as two GEMMs, the gather reading the k|v GEMM's output with no export copy, measured 0.25 % slower
+        # per CP = 8 rank forward in a same-process A/B: profiles/r5/cp_sim/split_qkv_ab_rejected.log)
         kv = torch.empty((n * B, 2 * D), dtype=BF16, device=self.device)
         N.copy_rows(qkv, 3 * D, kv, 2 * D, n * B, 2 * D, src_offset=D)
         kv_all = self._kv_gather_buffer((cp_size * n * B, 2 * D))
