@@ -192,6 +192,35 @@ def test_final_ln_mod(device):
     record("final layer LN-mod (cp25_final_ln_mod)", out, ref, truth, 1e-5)
 
 
+def test_fp32_linears(device):
+    """cp25_gemm_f32: the final layer's Linear(D, 64) over the tokens (minimal_v4_dit.py:993-995) and the AdaLN-LoRA
+    second layer with its LoRA addend (:1136-1154), against the reference's fp32 F.linear (torch's fp32 GEMM on the
+    same device; TF32 off) and float64."""
+    g = torch.Generator(device=device).manual_seed(8)
+    x = torch.randn(8192, 2048, generator=g, device=device)
+    w = torch.randn(64, 2048, generator=g, device=device) * 2048 ** -0.5
+    record("final linear fp32 (cp25_gemm_f32)", N.gemm_f32(x, w, split_k=False), F.linear(x, w),
+           x.double() @ w.double().t(), 1e-5)
+    a1 = torch.randn(62, 84 * 256, generator=g, device=device).view(62, 84, 256).transpose(0, 1)
+    w2 = torch.randn(84, 6144, 256, generator=g, device=device) * 256 ** -0.5
+    lora = torch.randn(62, 6144, generator=g, device=device)
+    record("AdaLN-LoRA layer 2 + LoRA fp32 (cp25_gemm_f32, batched)", N.gemm_f32(a1, w2, add=lora),
+           torch.bmm(a1, w2.transpose(1, 2)) + lora, torch.bmm(a1.double(), w2.double().transpose(1, 2)) + lora.double(),
+           1e-5)
+
+
+def test_layer_norm_affine(device):
+    """cp25_layer_norm: the cross-view net's affine LayerNorm (multiview_cross_dit.py:290, :441) against torch's bf16
+    F.layer_norm (the reference's op) and fp32."""
+    g = torch.Generator(device=device).manual_seed(9)
+    D = 2048
+    x = (torch.randn(4096, D, generator=g, device=device) * 2 + 0.5).to(BF16)
+    w = (1 + 0.2 * torch.randn(D, generator=g, device=device)).to(BF16)
+    b = (0.2 * torch.randn(D, generator=g, device=device)).to(BF16)
+    record("affine LayerNorm (cp25_layer_norm)", N.layer_norm(x, w, b), F.layer_norm(x, (D,), w, b, eps=1e-6),
+           F.layer_norm(x.float(), (D,), w.float(), b.float(), eps=1e-6), 2e-3)
+
+
 def test_vae_ops(device):
     """cp25_conv3d (CausalConv3d, wan2pt1.py:44-62), cp25_rms_norm_silu (RMS_norm + SiLU, :64-85),
     cp25_vae_attn (AttentionBlock core, :214-261)."""
