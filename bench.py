@@ -68,9 +68,6 @@ def parse():
                          "(dit.data_tight_k_bound; off by default)")
     ap.add_argument("--no-whole-video", action="store_true",
                     help="skip the end-to-end video (value is then the per-evaluation model; for quick A/B runs)")
-    ap.add_argument("--block-gemm", default="own", choices=("own", "lib"),
-                    help="bf16 block projections: own = the hand-written MFMA GEMM with fused GELU / gated-residual "
-                         "epilogues (default), lib = hipBLASLt + the elementwise kernels (A/B)")
     ap.add_argument("--no-cfg-share", action="store_true",
                     help="every CFG entry computes block 0's shared self-attention prefix (A/B of the sharing)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -178,7 +175,6 @@ def main():
                                 linear_precision=a.linear_precision, attention_precision=a.attention_precision)
     model = pipe.model
     model.net.share_cfg_block0 = not a.no_cfg_share
-    model.net.block_gemm = a.block_gemm
     model.net.data_tight_k_bound = a.data_tight_k_bound
     if a.norm_weights:
         lo, hi = (float(x) for x in a.norm_weights.split(","))
@@ -392,7 +388,6 @@ def main():
                 "linear_precision": a.linear_precision,
                 "attention_precision": a.attention_precision,
                 "cfg_block0_shared": bool(net.share_cfg_block0),
-                "block_gemm": net.block_gemm,
                 "norm_weights": a.norm_weights or "ones (init)",
                 "attention_kernels": kernels_metric,
                 "metric_config": valid,

@@ -101,7 +101,6 @@ SIGNATURES = {
     "cp25_rms_norm_silu": [_P, _P, _P, _I64, _I, _I, _P],
     "cp25_conv3d_select": [_I],
     "cp25_attn_cross_select": [_I],
-    "cp25_gemm_select": [_I],
     "cp25_softmax_rows": [_P, _I64, _I, _I64, _F, _P, _I64, _P],
     "cp25_vae_attn": [_P, _I64, _I64, _P, _I64, _I64, _P, _I64, _I64, _P, _I64, _I64, _I, _I, _I, _I, _F, _P, _I64,
                       _P],
@@ -321,11 +320,19 @@ def attn_cross_select(form: int) -> int:
     return rc
 
 
-def gemm_select(form: int) -> int:
-    """cp25_gemm_select: the bf16 block-GEMM kernel form, 0 = gemm_nt_8ph (8 waves of 128 x 64), 1 = gemm_nt_4w (4
-    waves of 128 x 128); bit-identical (the same MFMA chains in the same K order). Returns the previous form."""
-    rc = load_library().cp25_gemm_select(int(form))
-    _check("cp25_gemm_select", min(rc, 0))
+def attn_self_select(form: int) -> int:
+    """Lab builds only (tools/lab/w64/build_lab.sh, loaded through _LIB_PATH): cp25_attn_self_select, the kernel form
+    of prescaled bf16 self-attention launches, 0 = attn_fwd_m16 (the product kernel), 1 = attn_fwd_w64 in the zero- and
+    fixed-shift modes, 2 = attn_fwd_w64 in every mode (bit-identical). Returns the previous form."""
+    lib = load_library()
+    fn = getattr(lib, "cp25_attn_self_select", None)
+    if fn is None:
+        raise RuntimeError("cp25_attn_self_select: not in this libcp25.so (attn_fwd_w64 is a lab build, "
+                           "tools/lab/w64/build_lab.sh)")
+    fn.argtypes = [ctypes.c_int]
+    fn.restype = ctypes.c_int
+    rc = fn(int(form))
+    _check("cp25_attn_self_select", min(rc, 0))
     return rc
 
 
@@ -496,7 +503,7 @@ EPI_NONE, EPI_GELU, EPI_RES, EPI_HNORM, EPI_QKV = 0, 1, 2, 3, 4
 
 
 def gemm_supported(N: int, K: int) -> bool:
-    """Shapes cp25_gemm_epi is built for (N multiple of 256, K of 64); others stay on the library GEMM."""
+    """Shapes cp25_gemm_epi is built for (N multiple of 256, K of 64); the sampler raises ValueError for others."""
     return N % 256 == 0 and K % 64 == 0
 
 
@@ -663,7 +670,7 @@ def gemm_res(a: torch.Tensor, w: torch.Tensor, x: torch.Tensor, x_st: int, x_sb:
 
 
 def gemm_fp8_supported(N: int, K: int) -> bool:
-    """Shapes cp25_gemm_fp8 is built for (N multiple of 256, K of 256); others stay on torch._scaled_mm."""
+    """Shapes cp25_gemm_fp8 is built for (N multiple of 256, K of 256); the fp8 option raises ValueError for others."""
     return N % 256 == 0 and K % 256 == 0
 
 

@@ -201,6 +201,14 @@ class Geometry:
         return self.T * self.Hp * self.Wp
 
 
+def _require_gemm(w: torch.Tensor, what: str = "projection") -> None:
+    """Every linear of the sampler runs on a hand-written GEMM, with no library fallback: a weight [N, K] whose shape
+    cp25_gemm_epi is not built for (N a multiple of 256, K of 64) raises ValueError, as a missing libcp25.so does."""
+    n_out, k = w.shape
+    if not N.gemm_supported(n_out, k):
+        raise ValueError(f"{what} weight [{n_out}, {k}]: the own GEMM needs N % 256 == 0 and K % 64 == 0")
+
+
 def _rows(h, m: int):
     """[m, D] rows of an LN-mod output: a bf16 [n, B, D] tensor, or an fp8 (q, scale) pair as is."""
     return h if isinstance(h, tuple) else h.view(m, -1)
@@ -236,11 +244,6 @@ class MinimalV1LVGDiT:
         self.attention_precision = "bf16"
         # the CFG pair's shared block-0 prefix runs once (see _blocks); False: every entry computes it
         self.share_cfg_block0 = True
-        # bf16 block projections: "own" (default) = the hand-written MFMA GEMM with fused epilogues (cp25_gemm_epi:
-        # QKV, cross-q; + exact GELU on MLP layer1; cp25_gemm_res: the gated residual fused into the output,
-        # cross-output and MLP layer2 projections, so each LN-mod reads the new x once); "lib" = hipBLASLt GEMMs with
-        # the GELU and the residuals in the elementwise kernels (the round-2 path, kept for A/B)
-        self.block_gemm = "own"
         # single-GPU self-attention with weight-based norm bounds past the zero-shift window (trained q/k norm weights):
         # True: the k RMSNorm kernel measures max |k| (64 device slots) and the attention runs the gated pair, the
         # zero-shift loop for every 256-query block whose data-tight bound allows it (cp25_attn_fwd_prescaled_kslots).
@@ -261,8 +264,8 @@ class MinimalV1LVGDiT:
     def set_linear_precision(self, precision: str) -> None:
         """"bf16" (default, the reference's arithmetic) or "fp8": the 28 blocks' q/k/v, output, cross-q,
         cross-output and MLP projections run as fp8 (OCP E4M3) MFMA GEMMs, the hand-written cp25_gemm_fp8 (with the
-        gated residual fused into the output projections' epilogue, cp25_gemm_fp8_res; torch._scaled_mm for shapes it
-        is not built for or with block_gemm = "lib"), activations quantised per row by cp25_quant_fp8_rows (the MLP's
+        gated residual fused into the output projections' epilogue, cp25_gemm_fp8_res; a ValueError for shapes it is
+        not built for), activations quantised per row by cp25_quant_fp8_rows (the MLP's
         fused with its GELU, cp25_gelu_quant_fp8), weights per output channel (once, on first use). Embedders, AdaLN, the text projection and the final layer
         stay bf16/fp32. The reference has no fp8 path: the cost is stated against the bf16 path
         (DESIGN.md §4), not pinned to a reference output."""
@@ -349,17 +352,24 @@ class MinimalV1LVGDiT:
         return ent
 
     def _own(self, x, w: torch.Tensor) -> bool:
-        """The hand-written GEMM runs this projection: bf16 linears, shapes it is built for, block_gemm == "own"."""
-        return (self.block_gemm == "own" and not isinstance(x, tuple) and self.linear_precision == "bf16"
-                and N.gemm_supported(w.shape[0], w.shape[1]))
+        """True: a bf16 projection, on the hand-written bf16 GEMM (cp25_gemm_*); False: the fp8 option's operands.
+        Every projection runs on a hand-written GEMM: a weight shape it is not built for raises ValueError."""
+        if isinstance(x, tuple) or self.linear_precision != "bf16":
+            return False
+        _require_gemm(w)
+        return True
 
     def _own_fp8(self, w: torch.Tensor) -> bool:
-        """The hand-written fp8 GEMM runs this projection (fp8 option): shapes it is built for, block_gemm == "own"."""
-        return self.block_gemm == "own" and self.linear_precision == "fp8" and N.gemm_fp8_supported(w.shape[0], w.shape[1])
+        """True under the fp8 option (the hand-written cp25_gemm_fp8; ValueError for a shape it is not built for)."""
+        if self.linear_precision != "fp8":
+            return False
+        if not N.gemm_fp8_supported(w.shape[0], w.shape[1]):
+            raise ValueError(f"fp8 projection weight {tuple(w.shape)}: cp25_gemm_fp8 needs N and K multiples of 256")
+        return True
 
     def _fused_res(self, a, w: torch.Tensor, B: int, hw: int) -> int:
         """Which hand-written GEMM carries this projection's gated residual in its epilogue: 1 bf16 (cp25_gemm_res),
-        2 fp8 (cp25_gemm_fp8_res), 0 none (library GEMM, the residual in cp25_ln_mod / the final layer). Both need
+        2 fp8 (cp25_gemm_fp8_res), 0 none (the plain GEMM, the residual in cp25_ln_mod / the final layer). Both need
         16 % B == 0 and at least 16 / B tokens per frame (N.gemm_res_supported)."""
         if not N.gemm_res_supported(w.shape[0], w.shape[1], B, hw):
             return 0
@@ -389,8 +399,8 @@ class MinimalV1LVGDiT:
                   B: int, geo: "Geometry", n: int, lnk: dict, shift=None, scale=None, gelu_in: bool = False):
         """x' = x + gate * (a w^T) (Block.forward's gated residuals, minimal_v4_dit.py:1204, 1237, 1246) for the token-
         major [n, B, D] rows, then (if shift is given) h = LN-mod(x') for the next sub-layer. Own GEMM: the residual
-        rides in its epilogue (cp25_gemm_res) and the LN-mod reads x' only; else hipBLASLt + the residual in
-        cp25_ln_mod. Returns (x' [n, B, D], h or None)."""
+        rides in its epilogue (cp25_gemm_res) and the LN-mod reads x' only; else the plain own GEMM + the residual
+        in cp25_ln_mod. Returns (x' [n, B, D], h or None)."""
         D = w.shape[0]
         fused = None
         path = self._fused_res(a, w, B, geo.hw)
@@ -407,7 +417,7 @@ class MinimalV1LVGDiT:
                 h = N.ln_mod(x_new, shift, scale, x_st=B * D, x_sb=D, **dict(lnk, B=B))
             return x_new, h
         if shift is None:
-            raise ValueError("the library-GEMM path fuses the last residual into the final layer instead")
+            raise ValueError("the unfused-residual path fuses the last residual into the final layer instead")
         y = self._linear(a, w, key, gelu_in=gelu_in)
         x_new = torch.empty((n, B, D), dtype=BF16, device=self.device)
         h = N.ln_mod(x, shift, scale, x_st=x_st, x_sb=x_sb, y=y, gate=gate, x_out=x_new, **dict(lnk, B=B))
@@ -415,20 +425,20 @@ class MinimalV1LVGDiT:
 
     def _linear(self, x, w: torch.Tensor, key: str, gelu_in: bool = False) -> torch.Tensor:
         """y = x w^T for a block projection (x [M, K] bf16 contiguous, or an fp8 operand pair (q, scale)
-        that cp25_ln_mod_fp8 already produced). bf16: hipBLASLt bf16 GEMM (GELU, if asked, applied in
-        place to x first). fp8: row-quantised x (GELU fused) times the fp8 weight."""
+        that cp25_ln_mod_fp8 already produced). bf16: the own bf16 GEMM (GELU, if asked, applied in place to x
+        first). fp8: row-quantised x (GELU fused) times the fp8 weight on cp25_gemm_fp8."""
         if isinstance(x, tuple):
             q, s = x
         elif self.linear_precision == "bf16":
             if gelu_in:
                 N.gelu_(x)
-            return F.linear(x, w)
+            _require_gemm(w)
+            return N.gemm_epi(x, w)
         else:
             q, s = N.quant_fp8_rows(x, gelu=gelu_in)
+        self._own_fp8(w)
         w8, ws = self._fp8_weight(key, w)
-        if self._own_fp8(w):
-            return N.gemm_fp8(q, s, w8, ws)
-        return torch._scaled_mm(q, w8.t(), scale_a=s, scale_b=ws, out_dtype=BF16)
+        return N.gemm_fp8(q, s, w8, ws)
 
     # ---------------------------------------------------------------- loading
     def load_state_dict(self, state_dict: Dict[str, torch.Tensor], strict: bool = True) -> None:
@@ -543,10 +553,6 @@ class MinimalV1LVGDiT:
             # crossattn_proj = Linear + bias + exact GELU (minimal_v4_dit.py:1430-1434, applied at :1604); EPI_GELU
             # applies the GELU to the rounded sum (cp25_gelu's arithmetic)
             ctx = self._bias_linear(crossattn_emb.reshape(B * Lc, c_in), "crossattn_proj.0", N.EPI_GELU)
-            if ctx is None:
-                ctx = F.linear(crossattn_emb.to(device=self.device, dtype=BF16), p["crossattn_proj.0.weight"],
-                               p["crossattn_proj.0.bias"]).reshape(B * Lc, -1).contiguous()
-                N.gelu_(ctx)
         else:
             ctx = crossattn_emb.to(device=self.device, dtype=BF16).reshape(B * Lc, c_in).contiguous()
         H, hd = cfg.num_heads, cfg.head_dim
@@ -554,11 +560,12 @@ class MinimalV1LVGDiT:
         for i in range(cfg.num_blocks):
             # cross-attention k/v projections (minimal_v4_dit.py:401-404) of the text context, once per prompt
             wk, wv = p[f"blocks.{i}.cross_attn.k_proj.weight"], p[f"blocks.{i}.cross_attn.v_proj.weight"]
-            own = self.block_gemm == "own" and N.gemm_supported(wk.shape[0], wk.shape[1])
-            k = N.gemm_epi(ctx, wk) if own else F.linear(ctx, wk)
+            _require_gemm(wk, "cross-attention k_proj")
+            _require_gemm(wv, "cross-attention v_proj")
+            k = N.gemm_epi(ctx, wk)
             N.head_rmsnorm_rope(k, n_rows=B * Lc, B=1, H=H, head_off=0,
                                 weight=p[f"blocks.{i}.cross_attn.k_norm.weight"])
-            v = N.gemm_epi(ctx, wv) if own else F.linear(ctx, wv)
+            v = N.gemm_epi(ctx, wv)
             ks.append(k.view(B, Lc, H, hd))
             vs.append(v.view(B, Lc, H, hd))
         return ContextCache(B=B, k=ks, v=vs)
@@ -567,14 +574,16 @@ class MinimalV1LVGDiT:
         """bf16 nn.Linear with bias (weight / bias `key`.weight / .bias) of x [M, K] on the hand-written GEMM: the bias
         rides as one more K column (a' = [x | 1 | 0..], w' = [w | bias | 0..], K padded to a multiple of 64), so it
         enters the fp32 accumulator before the product's one bf16 rounding, as the library's bias epilogue adds it
-        (tests/test_gemm_f32_gpu.py: bit-identical to F.linear(bias) on its case). None where the GEMM is not built
-        for the shape (the caller runs F.linear)."""
+        (tests/test_gemm_f32_gpu.py: bit-identical to F.linear(bias) on its case). ValueError where the GEMM is not
+        built for the shape. The padded operand is a copy of x (for crossattn_proj: [B * 512, 100 416] bf16, ~0.2 GB,
+        once per prompt, freed on return)."""
         p = self.sd
         w, bias = p[key + ".weight"], p[key + ".bias"]
         n_out, k_in = w.shape
         kp = (k_in + 1 + 63) // 64 * 64
-        if self.block_gemm != "own" or not N.gemm_supported(n_out, kp):
-            return None
+        if not N.gemm_supported(n_out, kp):
+            raise ValueError(f"{key}: [{n_out}, {k_in}] + bias is not a shape the own GEMM is built for "
+                             "(N a multiple of 256)")
         wb = self._bias_w.get(key)
         if wb is None:
             wb = torch.zeros((n_out, kp), dtype=BF16, device=self.device)
@@ -621,14 +630,9 @@ class MinimalV1LVGDiT:
             a = a.reshape(Ba, 1, A * dim)
 
         def mlp(name):  # fc1 and fc2 (+ bias) on the hand-written GEMM, the tanh GELU between them in torch
-            x2 = a.reshape(-1, a.shape[-1])
-            h = self._bias_linear(x2, name + ".fc1")
-            if h is None:
-                h = F.linear(x2, p[name + ".fc1.weight"], p[name + ".fc1.bias"])
+            h = self._bias_linear(a.reshape(-1, a.shape[-1]), name + ".fc1")
             h = F.gelu(h, approximate="tanh")
             y = self._bias_linear(h, name + ".fc2")
-            if y is None:
-                y = F.linear(h, p[name + ".fc2.weight"], p[name + ".fc2.bias"])
             return y.view(*a.shape[:-1], -1)
 
         e_d, e_3d = mlp("action_embedder_B_D"), mlp("action_embedder_B_3D")
@@ -709,22 +713,21 @@ class MinimalV1LVGDiT:
         if not cfg.view_condition_dim:
             if rows_k128 and (Bx != 1 or f != 72 or patch_rows.stride(0) != 128 or patch_rows.stride(2) != 1):
                 raise ValueError("rows_k128: expected the [n, 1, 72] view of patchify(ld=128)'s [n, 128] buffer")
-            if self.block_gemm == "own" and N.gemm_supported(D, 128) and f <= 128:
-                # the zero-padded K = 128 operand of the own GEMM against the weight zero-padded to 128 columns (the
-                # same sums as K = 72): rows from patchify(ld=128) are that operand already, other rows are copied
-                # into it
-                if rows_k128:
-                    a = torch.as_strided(patch_rows, (n, 128), (128, 1))
-                else:
-                    a = torch.zeros((n * Bx, 128), dtype=BF16, device=self.device)
-                    a[:, :f] = patch_rows.reshape(n * Bx, f)
-                wp = self._x_embed_w128
-                if wp is None or wp.shape[0] != D:
-                    wp = torch.zeros((D, 128), dtype=BF16, device=self.device)
-                    wp[:, :f] = w[:, :f]
-                    self._x_embed_w128 = wp
-                return N.gemm_epi(a, wp).view(n, Bx, D)
-            return F.linear(patch_rows.reshape(n * Bx, f), w).view(n, Bx, D)
+            if f > 128 or not N.gemm_supported(D, 128):
+                raise ValueError(f"x_embedder [{D}, {f}]: the own GEMM takes f <= 128 features and D % 256 == 0")
+            # the zero-padded K = 128 operand of the own GEMM against the weight zero-padded to 128 columns (the same
+            # sums as K = 72): rows from patchify(ld=128) are that operand already, other rows are copied into it
+            if rows_k128:
+                a = torch.as_strided(patch_rows, (n, 128), (128, 1))
+            else:
+                a = torch.zeros((n * Bx, 128), dtype=BF16, device=self.device)
+                a[:, :f] = patch_rows.reshape(n * Bx, f)
+            wp = self._x_embed_w128
+            if wp is None or wp.shape[0] != D:
+                wp = torch.zeros((D, 128), dtype=BF16, device=self.device)
+                wp[:, :f] = w[:, :f]
+                self._x_embed_w128 = wp
+            return N.gemm_epi(a, wp).view(n, Bx, D)
         V = geo.n_views
         if view_indices is None:
             view_indices = torch.arange(V, device=self.device)
@@ -877,7 +880,8 @@ class MinimalV1LVGDiT:
         hv = N.layer_norm(x.view(n * B, D), p[pre + "layer_norm_cross_view_attn.weight"],
                           p[pre + "layer_norm_cross_view_attn.bias"])
         w = self.w_cv_qkv[i]
-        qkv = N.gemm_epi(hv, w) if self._own(hv, w) else F.linear(hv, w)
+        _require_gemm(w, "cross-view q|k|v")
+        qkv = N.gemm_epi(hv, w)
         q_scale, attn_kw = self._attn_mode(self.cvattn_bounds[i], hd)
         N.head_rmsnorm_rope(qkv, n_rows=n * B, B=B, H=H, head_off=0, weight=p[pre + "cross_view_attn.q_norm.weight"],
                             out_scale=q_scale)
@@ -1027,10 +1031,8 @@ class MinimalV1LVGDiT:
                 # layer1 + exact-erf GELU in one hand-written MFMA GEMM (the epilogue applies it to the bf16 product, as
                 # cp25_gelu would): the [n B, 4 D] hidden makes one HBM trip instead of three
                 u = N.gemm_epi(h1, w1, epilogue=N.EPI_GELU)
-            else:
+            else:  # fp8 option: the GELU rides in layer2's row quantisation
                 u = self._linear(h1, w1, pre + "mlp.layer1")
-                if self.linear_precision == "bf16":
-                    N.gelu_(u)
             if self._fused_res(u, w2, B, geo.hw):
                 x, h = self._proj_res(u, w2, pre + "mlp.layer2", x, B * D, D, g_ml, B, geo, n, lnk, sh, sc,
                                       gelu_in=self.linear_precision == "fp8")

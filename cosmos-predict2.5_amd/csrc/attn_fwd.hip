@@ -19,119 +19,10 @@
 // NaN inputs are not supported (built with -fno-honor-nans; the reference's flash kernels do not define NaN
 // propagation either). Numerics: scores, shifts and sums fp32, P rounded to bf16 before P.V (as every flash kernel
 // the reference dispatches to does), O accumulated in fp32, normalised and rounded once to bf16.
-#include "cp25_common.h"
-
-#include <algorithm>
-#include <type_traits>
+#include "attn_common.h"
 
 namespace {
-
-constexpr int kD = 128;        // head dim
-constexpr int kWaves = 8;      // waves per workgroup
-constexpr int kQRows = 32;     // query rows per wave
-constexpr int kQBlk = kWaves * kQRows;  // 256 query rows per workgroup
-constexpr int kKBlk = 64;      // keys per tile
-constexpr int kThreads = kWaves * 64;
-// Softmax-shift ranges (log2 units). A term is 2^(s - shift) <= 2^kTop, so a row sum is <= Lk 2^96 and O = sum P v is
-// <= Lk 2^96 max|v|: inside fp32 (2^128) while max|v| Lk < 2^32, e.g. |v| < 2.6e4 at config 4's Lk = 163 800 (the
-// DiT's v is a bf16 projection of a normalised row, orders of magnitude smaller; checked at the top of the window
-// over 163 840 keys with |v| ~ 400 by tests/test_attn_m16_gpu.py::test_m16_zero_shift_top_of_window_long_keys). The
-// contract guard below poisons a row whose sum overflows. bf16 P has the fp32 exponent range.
-constexpr float kTop = 96.f;        // zero / fixed shift: largest exponent a term may reach
-constexpr float kMaxBound = 98.f;   // fixed shift: largest score bound b (smallest row-max term 2^(96 - 2 b) >= 2^-100)
-constexpr float kTopF8 = 60.f;      // fp8 Q K^T form: P = exp2(S) unshifted for bound products up to this
-constexpr float kLazy = 24.f;       // online max: rescale only when a row max exceeds the shift by more (P <= 2^24)
-
-typedef __attribute__((address_space(3))) const char* lds_char_ptr;
-
-// cp25_common.h's hn_* pieces on element pairs (v_pk_* f32): per element the same IEEE operations, contraction off
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f32x2 hn2_sumsq8(const f32x2* x) {  // two sequential 8-term chains
-#pragma clang fp contract(off)
-  f32x2 ss = {0.f, 0.f};
-#pragma unroll
-  for (int e = 0; e < 8; ++e) ss += x[e] * x[e];
-  return ss;
-}
-__device__ __forceinline__ f32x2 hn2_norm(f32x2 x, f32x2 rstd, f32x2 w) {
-#pragma clang fp contract(off)
-  const f32x2 t = (x * rstd) * w;
-  return __builtin_convertvector(__builtin_convertvector(t, bf16x2v), f32x2);  // rbf
-}
-__device__ __forceinline__ f32x2 hn2_rope(f32x2 v, f32x2 partner, float sgn, f32x2 c, f32x2 s) {
-#pragma clang fp contract(off)
-  const f32x2 sg = {sgn, sgn};
-  return __builtin_elementwise_fma(v, c, (sg * partner) * s);
-}
-
-// compile-time loop: f(integral_constant<int, I>) for I = 0 .. N-1, in order
-template <int N, int I = 0, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for<N, I + 1>(f);
-  }
-}
-
-// The lane index computed afresh where it is used (opaque to CSE / loop-invariant hoisting): the persistent form
-// recomputes its lane-dependent addresses per use instead of holding them in VGPRs across the tile loop, where a
-// 256-VGPR kernel would spill them and reload them behind a vmcnt(0) that drains the tile loads in flight.
-__device__ __forceinline__ int lane_fresh() {
-  int l;
-  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-  return l;
-}
-
-__device__ __forceinline__ float wave_swap_sum(float x) {  // lanes l and l ^ 32
-  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-__device__ __forceinline__ float group4_sum(float x) {  // over the 4 lane groups of 16 (lanes c, c+16, c+32, c+48)
-  x += __shfl_xor(x, 16);
-  return x + __shfl_xor(x, 32);
-}
-__device__ __forceinline__ float group4_max(float x) {  // the same reduction by row swaps (no LDS crossbar)
-  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  x = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-  auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1]));
-}
-
-struct AttnArgs {
-  const unsigned short* q; const unsigned short* k; const unsigned short* v; unsigned short* o;
-  int64_t q_sb, q_sl, q_sh;
-  int64_t k_sb, k_sl, k_sh;
-  int64_t v_sb, v_sl, v_sh;
-  int64_t o_sb, o_sl, o_sh;
-  int B, H, Lq, Lk;
-  int nqb;          // query blocks per (b, h)
-  int nsplit;       // key-range splits per (b, h, query block) (1: O written directly)
-  int tps;          // key tiles per split
-  int ntk_v;        // fp8 P.V: key tiles per (b, h) of the v8t layout (ceil(Lk / 64))
-  const float* v_amax;  // fp8 P.V: per-(b, h) max |v| (v8t holds v * 448 / amax)
-  float s_init;     // fp8 forms: the Q K^T chains' initial C (-shift: P = exp2(S - shift) stays inside e5m2)
-  float* o_part;    // nsplit > 1: [nsplit][B][H][Lq][128] fp32 partial O (normalised per split)
-  float* lse_part;  // nsplit > 1: [nsplit][B][H][Lq] fp32 log2-sum-exp2 of the scaled scores
-  float scale_log2; // softmax scale * log2(e) (1 for a pre-scaled q)
-  float kbound;     // > 0: upper bound of |k| over all keys (fixed shift where it allows); 0: online max only
-  const float* kslots;  // gated pair: max |k| over all keys = the max of n_kslots floats kslots[32 i] (device memory)
-  int n_kslots;
-  // in-kernel q normalisation (cp25_attn_fwd_prescaled_qnorm, per-block forms): q holds the raw projection; each
-  // workgroup applies the per-head RMSNorm (weight qn_w[128], eps), the rotate-half RoPE of token qn_row0 + row
-  // (qn_cos / qn_sin [tokens][64] fp32; nullptr: none) and the factor qn_scale to its Q fragments as they load.
-  const unsigned short* qn_w;
-  const float* qn_cos;
-  const float* qn_sin;
-  float qn_eps, qn_scale;
-  int qn_row0;
-#ifdef CP25_ATTN_PROBE
-  // lab build only (tools/attn_probe.py; the product build has no stamp): [probe_wg][8 waves][32 tiles][4] s_memtime
-  // stamps of workgroups blockIdx.x < probe_wg, tiles probe_t0 .. probe_t0 + 31
-  unsigned long long* probe;
-  int probe_t0, probe_wg;
-#endif
-};
+using namespace cp25attn;
 
 // ------------------------------------------------------------------------------------------------
 // attn_fwd_m16. Fragments (lane l, g = l >> 4, c = l & 15), per wave and 64-key tile:
@@ -167,17 +58,12 @@ struct AttnArgs {
 //          and the rescale run only when a lane's own tile max crosses the threshold (rare after tile 0; rows below it
 //          take the branch with d = 0, exactly, so rows stay independent of each other).
 // The host picks the mode from the bounds (m16_mode).
-constexpr int kKStride16 = 288;
-constexpr int kVStride16 = 288;
 // MFMA phase: operand pairs read ahead of their MFMAs (attn_fwd_m16's kAhead): 3 (a ring of 4 fragments) in the
 // per-block forms, 2 in the persistent cross-attention. Round 3 (register-path staging): 2 freed the 4 VGPRs the online
 // form spilled in its loop at 3 (-3.4 %), zero shift -0.1 %, 4: online +7 % (profiles/r3/attn_nop/ring_depth_ab.log,
 // ring_depth2_ab.log). Round 5: with K and V staged by LDS-DMA the loops hold 3 without spills: online -0.4..-0.9 %,
 // zero shift (with its V by DMA too) -0.25 % (profiles/r5/attn_iso/, profiles/r5/attn_ab/).
 constexpr int kAheadDefault = 2;
-constexpr int kKBuf16 = kKBlk * kKStride16;        // 18432
-constexpr int kVBuf16 = kKBlk * kVStride16;        // 18432
-constexpr int kLds16 = 2 * kKBuf16 + 2 * kVBuf16;  // 73728
 
 // Persistent short-key form (kPersist, text cross-attention): one workgroup per CU walks a contiguous run of
 // (b, h, query block) blocks as ONE stream of key tiles (tile t = key tile t mod ntk of the run's block t / ntk), so
@@ -1468,12 +1354,34 @@ int m16_mode(float q_norm_bound, float k_norm_bound, float scale_log2, bool pres
 // per block. Set only through cp25_attn_cross_select (never read from the environment).
 int g_xattn_form = 1;
 
+#ifdef CP25_LAB_W64
+// Lab build only (tools/lab/w64/build_lab.sh): attn_fwd_w64, one wave per SIMD owning 64 query rows,
+// for prescaled self-attention launches (Lk > 4096, bf16, not the gated pair): g_self_form 1 = w64 in the zero- and
+// fixed-shift modes, 2 = w64 in every mode, 0 = attn_fwd_m16 (the product kernel) in every mode. Bit-identical to
+// attn_fwd_m16; measured 0.6 % slower inside the DiT (2.4 % with trained-size norm weights), so not in the product.
+int g_self_form = 1;
+bool use_w64(bool prescaled, bool short_keys, int mode) {
+  return prescaled && !short_keys && (g_self_form == 2 || (g_self_form == 1 && mode != 2));
+}
+#else
+constexpr bool use_w64(bool, bool, int) { return false; }
+#endif
+
 // the persistent form runs unsplit cross-attention launches in the zero-shift and online modes with >= 2 key tiles
 bool use_xattn_persistent(bool short_keys, int n_split, int mode, int64_t ntiles) {
   return g_xattn_form == 1 && short_keys && n_split == 1 && mode != 0 && ntiles >= 2;
 }
 
 }  // namespace
+
+#ifdef CP25_LAB_W64
+extern "C" int cp25_attn_self_select(int form) {  // (lab build only, see g_self_form)
+  if (form < 0 || form > 2) return CP25_ERR_INVAL;
+  const int prev = g_self_form;
+  g_self_form = form;
+  return prev;
+}
+#endif
 
 extern "C" int cp25_attn_cross_select(int form) {
   if (form != 0 && form != 1) return CP25_ERR_INVAL;
@@ -1587,6 +1495,7 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
     void (*kern)(AttnArgs) = nullptr;
     void (*kern_tail)(AttnArgs) = nullptr;  // the tail segments' symbol (plan_tail: self-attention shapes only)
     int64_t grid = nwg;
+    int threads = kThreads;
     if (prescaled && kslots && mode != 1) {
       // the gated pair: blocks whose data-tight bound allows it run the zero-shift loop, the others the online max
       hipLaunchKernelGGL((xk ? attn_fwd_m16<1, true, 1, false, 1> : attn_fwd_m16<0, true, 1, false, 1>),
@@ -1601,6 +1510,13 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
     } else {
 #define M16(P, M) kern = xk ? attn_fwd_m16<1, P, M> : attn_fwd_m16<0, P, M>; \
                   kern_tail = attn_fwd_m16<0, P, M, false, 0, 1>
+#ifdef CP25_LAB_W64
+      if (use_w64(prescaled, xk, mode)) {
+        kern = w64_kernel(mode, false);
+        kern_tail = w64_kernel(mode, true);
+        threads = kW64Threads;
+      } else
+#endif
       if (prescaled) {
         if (mode == 2) { M16(true, 2); } else if (mode == 1) { M16(true, 1); } else { M16(true, 0); }
       } else {
@@ -1609,7 +1525,7 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
 #undef M16
       if (n_tail) grid = nwg - nwg % num_cus();  // whole rounds; the rest below
     }
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kThreads), 0, stream, a);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(threads), 0, stream, a);
     CP25_LAUNCH_CHECK();
     // tail segments: (b, h) = bh, query blocks [qb_lo, qb_lo + nblk), as a B = H = 1 problem of s key-range splits on
     // the same kernel, its fp32 partials in the workspace, merged into o (the same arithmetic as any split launch)
@@ -1630,7 +1546,7 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
       t.tps = (int)cdiv(ntiles, g.s);
       t.o_part = (float*)workspace;
       t.lse_part = (float*)workspace + (size_t)g.s * t.Lq * kD;
-      hipLaunchKernelGGL(kern_tail, dim3((unsigned)(g.nblk * g.s)), dim3(kThreads), 0, stream, t);
+      hipLaunchKernelGGL(kern_tail, dim3((unsigned)(g.nblk * g.s)), dim3(threads), 0, stream, t);
       CP25_LAUNCH_CHECK();
       hipLaunchKernelGGL(attn_merge_splits, dim3((unsigned)cdiv((int64_t)t.Lq * 32, 256)), dim3(256), 0, stream,
                          t.o_part, t.lse_part, t.o, g.s, 1, 1, t.Lq, a.o_sb, a.o_sl, a.o_sh);
@@ -1766,6 +1682,11 @@ extern "C" const char* cp25_attn_kernel(int Lk, float softmax_scale, float q_nor
       return mode == 1 ? "attn_fwd_m16<cross, prescaled, zero shift, persistent>"
                        : (prescaled ? "attn_fwd_m16<cross, prescaled, online max, persistent>"
                                     : "attn_fwd_m16<cross, online max, persistent>");
+  }
+  if (fp8 == 0 && prescaled == 1 && use_w64(true, Lk <= 4096, m16_mode(q_norm_bound, k_norm_bound, 1.f, true))) {
+    static const char* w64[3] = {"attn_fwd_w64<self, prescaled, fixed shift>", "attn_fwd_w64<self, prescaled, zero shift>",
+                                 "attn_fwd_w64<self, prescaled, online max>"};
+    return w64[m16_mode(q_norm_bound, k_norm_bound, 1.f, true)];
   }
   static const char* names[2][2][3] = {
       {{"attn_fwd_m16<self, fixed shift>", "?", "attn_fwd_m16<self, online max>"},

@@ -720,472 +720,7 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
     __builtin_amdgcn_s_barrier();
   }
 }
-
-// ---------------------------------------------------------------------------------------------------------------
-// gemm_nt_4w (round 5): one wave per SIMD, each wave a 128 x 128 block of the 256 x 256 output tile (kTM = 256; a
-// 64 x 128 block of a 128 x 256 tile with kTM = 128, the tail rounds of the tile plan below), 256 accumulators per lane
-// (the accumulator file) and the whole 512-register budget. Against gemm_nt_8ph's 8 waves of 128 x 64 a wave reads
-// 16 fragments per 64 MFMAs instead of 12 per 32: 1.5x fewer LDS bytes per FLOP (64 vs 42.7 FLOP per LDS byte), the
-// layout hipBLASLt's MT256x256x64 kernel uses, and no ping-pong barriers. Same LDS image (XOR
-// swizzle on the source side), same DMA pieces, same MFMA chains in the same K order as gemm_nt_8ph: bit-identical.
-// Per 64-deep K-tile kt (stage kt & 1), each wave:
-//   1. reads the K-tile's second 32-deep substep (16 ds_read_b128) into f[1];
-//   2. issues the first substep's 64 MFMAs from f[0];
-//   3. waits for its own K-tile kt+1 pieces (vmcnt(0): they are the only loads in flight) and the LDS reads, then one
-//      barrier: every wave's pieces of kt+1 have landed and every wave is done reading stage kt & 1;
-//   4. reads K-tile kt+1's first substep into f[0] and queues K-tile kt+2's DMA into stage kt & 1 (one piece per 4
-//      MFMAs of step 5), and
-//   5. issues the second substep's 64 MFMAs from f[1].
-// Persistent over tiles with the pipelined seam of gemm_nt_8ph: the C tile goes through the LDS into registers, the next
-// tile's K-tiles 0 and 1 are queued, then the epilogue math and the C stores run while they land.
-// Epilogue thread layout: thread t owns the 16-B chunk t % 32 of rows t / 32 + 8 it (it < kTM / 8), i.e. the same
-// lane-per-chunk layout as gemm_nt_8ph (16 lanes = one 128-column head of a row), 8 rows apart instead of 16.
-// every accumulator register, as an asm clobber list (gemm_nt_4w owns the accumulator file)
-#define CP25_ALL_AGPRS \
-  "a0", "a1", "a2", "a3", "a4", "a5", "a6", "a7", "a8", "a9", "a10", "a11", "a12", "a13", "a14", "a15", "a16", \
-  "a17", "a18", "a19", "a20", "a21", "a22", "a23", "a24", "a25", "a26", "a27", "a28", "a29", "a30", "a31", "a32", \
-  "a33", "a34", "a35", "a36", "a37", "a38", "a39", "a40", "a41", "a42", "a43", "a44", "a45", "a46", "a47", "a48", \
-  "a49", "a50", "a51", "a52", "a53", "a54", "a55", "a56", "a57", "a58", "a59", "a60", "a61", "a62", "a63", "a64", \
-  "a65", "a66", "a67", "a68", "a69", "a70", "a71", "a72", "a73", "a74", "a75", "a76", "a77", "a78", "a79", "a80", \
-  "a81", "a82", "a83", "a84", "a85", "a86", "a87", "a88", "a89", "a90", "a91", "a92", "a93", "a94", "a95", "a96", \
-  "a97", "a98", "a99", "a100", "a101", "a102", "a103", "a104", "a105", "a106", "a107", "a108", "a109", "a110", \
-  "a111", "a112", "a113", "a114", "a115", "a116", "a117", "a118", "a119", "a120", "a121", "a122", "a123", "a124", \
-  "a125", "a126", "a127", "a128", "a129", "a130", "a131", "a132", "a133", "a134", "a135", "a136", "a137", "a138", \
-  "a139", "a140", "a141", "a142", "a143", "a144", "a145", "a146", "a147", "a148", "a149", "a150", "a151", "a152", \
-  "a153", "a154", "a155", "a156", "a157", "a158", "a159", "a160", "a161", "a162", "a163", "a164", "a165", "a166", \
-  "a167", "a168", "a169", "a170", "a171", "a172", "a173", "a174", "a175", "a176", "a177", "a178", "a179", "a180", \
-  "a181", "a182", "a183", "a184", "a185", "a186", "a187", "a188", "a189", "a190", "a191", "a192", "a193", "a194", \
-  "a195", "a196", "a197", "a198", "a199", "a200", "a201", "a202", "a203", "a204", "a205", "a206", "a207", "a208", \
-  "a209", "a210", "a211", "a212", "a213", "a214", "a215", "a216", "a217", "a218", "a219", "a220", "a221", "a222", \
-  "a223", "a224", "a225", "a226", "a227", "a228", "a229", "a230", "a231", "a232", "a233", "a234", "a235", "a236", \
-  "a237", "a238", "a239", "a240", "a241", "a242", "a243", "a244", "a245", "a246", "a247", "a248", "a249", "a250", \
-  "a251", "a252", "a253", "a254", "a255"
-constexpr int k4wThreads = 256;
-
-template <int kEpi, int kTM>
-__global__ void __launch_bounds__(k4wThreads, 1)
-gemm_nt_4w(const unsigned short* __restrict__ A, int64_t lda, const unsigned short* __restrict__ W, int64_t ldw,
-           unsigned short* __restrict__ C, int64_t ldc, int M, int N, int K, ResEpi re) {
-  static_assert(kTM == 256 || kTM == 128, "row tile");
-  constexpr int kWM = kTM / 2;       // wave rows
-  constexpr int kFI = kWM / 16;      // A fragments per wave and substep (8 or 4)
-  constexpr int kAB = kTM * 128;     // A image bytes per stage (rows of 128 B = 64 bf16)
-  constexpr int kStg = kAB + 256 * 128;
-  constexpr int kPA = kTM / 32;      // A pieces per wave and K-tile (8 or 4)
-  constexpr int kPB = 8;             // W pieces per wave and K-tile
-  constexpr int kPieces = kPA + kPB;
-  constexpr int kRows = kTM / 8;     // epilogue rows per thread
-  constexpr int kLdsMain = 2 * kStg > kTM * 512 ? 2 * kStg : kTM * 512;
-  __shared__ __attribute__((aligned(16))) char smem[kLdsMain + (kEpi == CP25_EPI_GELU ? 2 * kGeluTab : 0)];
-
-  const int mt = (M + kTM - 1) / kTM, nt = N / kBN;
-  const int n_tiles = mt * nt;
-  const int nk = K / kBK;  // 64-deep K-tiles (even: host-checked)
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int my_slot = xcd_remap(blockIdx.x, gridDim.x);
-  const int gm = N >= 8192 ? 16 : kGroupM;  // L2 grouping of row tiles (as gemm_nt_8ph)
-  auto tile_mn = [&](int tile, int& m0, int& n0) __attribute__((always_inline)) {
-    const int group = tile / (gm * nt);
-    const int first_m = group * gm;
-    const int gsize = min(mt - first_m, gm);
-    m0 = (first_m + (tile % (gm * nt)) % gsize) * kTM;
-    n0 = ((tile % (gm * nt)) / gsize) * kBN;
-  };
-
-  // ---- DMA: wave w moves pieces w + 4 q (8 rows each) of the A and W images; piece p, lane l: row 8 p + l / 8, LDS
-  // chunk l % 8, global chunk (l % 8) ^ swz(row), swz(row) = (row >> 1) & 7 = (4 (w & 1) + (l / 8) / 2) & 7 for every
-  // piece of the wave (p and w agree mod 2), so one lane offset per operand; the piece row offset rides in soffset
-  const int prow = lane >> 3, ppos = lane & 7;
-  const int pc = ppos ^ ((4 * (wave & 1) + (prow >> 1)) & 7);
-  const int a_vo = prow * (int)lda * 2 + pc * 16, w_vo = prow * (int)ldw * 2 + pc * 16;
-  __amdgpu_buffer_rsrc_t a_rsrc, w_rsrc;
-  auto set_tile = [&](int m0, int n0) __attribute__((always_inline)) {
-    a_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (int64_t)m0 * lda), (short)0,
-                                               (int)((int64_t)min(M - m0, kTM) * lda * 2), 0x00020000);
-    w_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(W + (int64_t)n0 * ldw), (short)0, (int)((int64_t)kBN * ldw * 2),
-                                               0x00020000);
-  };
-  auto dma_piece = [&](int q, int kt, int stage) __attribute__((always_inline)) {  // q < kPieces: A pieces, then W
-    char* st = smem + stage * kStg;
-    if (q < kPA) {  // (q is a constant at every call site)
-      const int p = wave + 4 * q;
-      dma16(a_rsrc, (lds_void_ptr)(st + p * 1024), a_vo, p * 8 * (int)lda * 2 + kt * kBK * 2);
-    } else {
-      const int p = wave + 4 * (q - kPA);
-      dma16(w_rsrc, (lds_void_ptr)(st + kAB + p * 1024), w_vo, p * 8 * (int)ldw * 2 + kt * kBK * 2);
-    }
-  };
-  auto dma_ktile = [&](int kt, int stage) __attribute__((always_inline)) {
-#pragma unroll
-    for (int q = 0; q < kPieces; ++q) dma_piece(q, kt, stage);
-  };
-
-  // ---- fragments: lane (fr = l % 16, fg = l / 16) reads row fr of a 16-row block, k-chunk 4 s + fg (swizzled)
-  const int fr = lane & 15, fg = lane >> 4;
-  const int foff0 = fr * 128 + 16 * ((0 + fg) ^ ((fr >> 1) & 7));
-  const int foff1 = fr * 128 + 16 * ((4 + fg) ^ ((fr >> 1) & 7));
-  bf16x8 fa[2][kFI], fb[2][8];
-  // The accumulators live in the accumulator file under literal names, accumulator (i, j) in a[4 (8 i + j) .. + 3]:
-  // with C++ accumulator values the register allocator rotated them through copies and scratch (hundreds of moves per
-  // K-tile pair). Every AGPR is declared clobbered once at entry (the kernel descriptor allocates the file); the
-  // compiler keeps its own values in the arch VGPRs (audited: tests/test_isa_cpu.py, no compiler v_accvgpr outside the
-  // asm statements and no spill).
-  asm volatile("" ::: CP25_ALL_AGPRS);
-  auto read_sub = [&](auto sc, auto bc) __attribute__((always_inline)) {  // substep s of stage BUF -> fa[s], fb[s]
-    constexpr int S = decltype(sc)::value, BUF = decltype(bc)::value;
-    const char* st = smem + BUF * kStg;
-    const int fo = S ? foff1 : foff0;
-#pragma unroll
-    for (int i = 0; i < kFI; ++i) fa[S][i] = *reinterpret_cast<const bf16x8*>(st + (wm * kWM + 16 * i) * 128 + fo);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) fb[S][j] = *reinterpret_cast<const bf16x8*>(st + kAB + (wn * 128 + 16 * j) * 128 + fo);
-  };
-  // the 8 kFI MFMAs of substep S (ZC: the tile's first, C = 0); with dma_kt >= 0 the K-tile's DMA pieces ride between
-  // them, one per kDmaEvery MFMAs. The asm MFMAs get no compiler hazard padding: the accumulators' only other readers
-  // and writers (the C staging) sit behind explicit s_nops
-  constexpr int kDmaEvery = (kFI * 8) / kPieces;  // 4 (kTM 256: 16 pieces over 64 MFMAs) or 2 (128: 12 over 32)
-  auto mfma_sub = [&](auto sc, auto ZC, int dma_kt, int dma_stage) __attribute__((always_inline)) {
-    constexpr int S = decltype(sc)::value;
-    // groups of kDmaEvery MFMAs (one row block i, columns j0 ..) per asm statement, then the group's DMA piece: hipcc
-    // pads every asm boundary with an s_nop, so one statement per MFMA paid a pad per MFMA. Every statement clobbers
-    // the whole accumulator file, so the compiler keeps nothing of its own there across one.
-    static_for<kFI * 8 / kDmaEvery>([&](auto GC) __attribute__((always_inline)) {
-      constexpr int g = decltype(GC)::value, n0 = g * kDmaEvery, i = n0 / 8, j0 = n0 % 8;
-      constexpr bool zc = decltype(ZC)::value;
-#define CP25_MF(A, B, R) "v_mfma_f32_16x16x32_bf16 a[%" #R ":%" #R "+3], %" #A ", %" #B ", "
-      if constexpr (kDmaEvery == 4) {
-        if constexpr (zc)
-          asm volatile(CP25_MF(0, 1, 5) "0\n\t" CP25_MF(0, 2, 6) "0\n\t" CP25_MF(0, 3, 7) "0\n\t" CP25_MF(0, 4, 8) "0"
-                       ::"v"(fa[S][i]), "v"(fb[S][j0]), "v"(fb[S][j0 + 1]), "v"(fb[S][j0 + 2]), "v"(fb[S][j0 + 3]),
-                       "i"(4 * n0), "i"(4 * n0 + 4), "i"(4 * n0 + 8), "i"(4 * n0 + 12) : CP25_ALL_AGPRS);
-        else
-          asm volatile(CP25_MF(0, 1, 5) "a[%5:%5+3]\n\t" CP25_MF(0, 2, 6) "a[%6:%6+3]\n\t" CP25_MF(0, 3, 7)
-                       "a[%7:%7+3]\n\t" CP25_MF(0, 4, 8) "a[%8:%8+3]"
-                       ::"v"(fa[S][i]), "v"(fb[S][j0]), "v"(fb[S][j0 + 1]), "v"(fb[S][j0 + 2]), "v"(fb[S][j0 + 3]),
-                       "i"(4 * n0), "i"(4 * n0 + 4), "i"(4 * n0 + 8), "i"(4 * n0 + 12) : CP25_ALL_AGPRS);
-      } else {
-        static_assert(kDmaEvery == 2, "MFMA group");
-        if constexpr (zc)
-          asm volatile(CP25_MF(0, 1, 3) "0\n\t" CP25_MF(0, 2, 4) "0"
-                       ::"v"(fa[S][i]), "v"(fb[S][j0]), "v"(fb[S][j0 + 1]), "i"(4 * n0), "i"(4 * n0 + 4)
-                       : CP25_ALL_AGPRS);
-        else
-          asm volatile(CP25_MF(0, 1, 3) "a[%3:%3+3]\n\t" CP25_MF(0, 2, 4) "a[%4:%4+3]"
-                       ::"v"(fa[S][i]), "v"(fb[S][j0]), "v"(fb[S][j0 + 1]), "i"(4 * n0), "i"(4 * n0 + 4)
-                       : CP25_ALL_AGPRS);
-      }
-#undef CP25_MF
-      if constexpr (g < kPieces) {
-        if (dma_kt >= 0) dma_piece(g, dma_kt, dma_stage);  // (constant-folded per call site)
-      }
-      // program order = issue order
-      __builtin_amdgcn_sched_barrier(0);
-    });
-  };
-
-  int tile = my_slot;
-  if (tile >= n_tiles) return;
-  u32x4 nwv = {0u, 0u, 0u, 0u};  // HNORM / QKV: this lane's 8 norm weights (columns 8 (ch & 15) .. of its head)
-  if constexpr (kEpi == CP25_EPI_HNORM || kEpi == CP25_EPI_QKV) nwv = *reinterpret_cast<const u32x4*>(re.nw + (tid & 15) * 8);
-  if constexpr (kEpi == CP25_EPI_GELU) {
-    unsigned short* tab = reinterpret_cast<unsigned short*>(smem + kLdsMain);
-    for (int i = tid; i < kGeluTab; i += k4wThreads) {
-      const int r = i % (kGeluNE * 128);
-      const unsigned u = (unsigned)(i / (kGeluNE * 128)) << 15 | (unsigned)(kGeluE0 + r / 128) << 7 | (unsigned)(r % 128);
-      tab[i] = f2bf(gelu_exact(bf2f((unsigned short)u)));
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  }
-  int m0, n0;
-  tile_mn(tile, m0, n0);
-  set_tile(m0, n0);
-  dma_ktile(0, 0);
-  dma_ktile(1, 1);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kPieces) : "memory");  // K-tile 0
-  __builtin_amdgcn_s_barrier();
-  bool stores_pending = false;
-
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  const int ch = tid & 31, r0 = tid >> 5;
-  while (true) {
-    read_sub(I0{}, I0{});
-    // one K-tile; BUF = its stage. kt + 1 < nk: K-tile kt + 1 is in flight into the other stage; kt + 2 < nk: it is
-    // queued here, into this stage. One loop with wave-uniform branches (peeled tail K-tiles made the register
-    // allocator permute the 256 accumulators at the loop exit)
-    auto ktile = [&](auto bc, int kt) __attribute__((always_inline)) {
-      constexpr int BUF = decltype(bc)::value;
-      read_sub(I1{}, bc);
-      if (BUF == 0 && kt == 0)
-        mfma_sub(I0{}, std::true_type{}, -1, 0);  // the tile's first products: C = 0
-      else
-        mfma_sub(I0{}, std::false_type{}, -1, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (kt + 1 < nk) {
-        if (kt == 0 && stores_pending)  // the previous tile's kRows C stores may still be in flight
-          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(kRows) : "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);  // no LDS read of the next K-tile above the barrier
-      if (kt + 1 < nk) read_sub(I0{}, std::integral_constant<int, BUF ^ 1>{});
-      if (kt + 2 < nk)
-        mfma_sub(I1{}, std::false_type{}, kt + 2, BUF);
-      else
-        mfma_sub(I1{}, std::false_type{}, -1, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    for (int kt = 0; kt < nk; kt += 2) {
-      ktile(I0{}, kt);
-      ktile(I1{}, kt + 1);
-    }
-    // an MFMA's D -> a non-MFMA reader needs the XDL write's wait states (8-pass: 12; the asm MFMAs get no compiler
-    // padding): the accumulators are read below
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_nop 15" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    // every wave's reads of this tile were done before the last K-tile's barrier and no DMA is in flight: the LDS
-    // becomes the C tile
-    const int next = tile + gridDim.x;
-    const bool has_next = next < n_tiles;
-    // CP25_EPI_RES: this thread's x chunks are requested now, into the registers the fragments held, so their HBM
-    // latency runs under the C staging (rows r0 + 8 it: token tok_a + it (8 / B), batch entry b; rows past M read the
-    // thread's first valid row and are not stored)
-    u32x4 xres[kEpi == CP25_EPI_RES ? kRows : 1];
-    if constexpr (kEpi == CP25_EPI_RES) {
-      const int row_a = min(m0 + r0, M - 1), tok_a = row_a / re.B, b = row_a % re.B, dtok = 8 / re.B;
-      const unsigned short* xp = re.x + (int64_t)tok_a * re.x_st + b * re.x_sb + n0 + ch * 8;
-      const int n_valid = (M - 1 - row_a) / 8;
-#pragma unroll
-      for (int it = 0; it < kRows; ++it)
-        xres[it] = *reinterpret_cast<const u32x4*>(xp + (int64_t)(it * dtok) * re.x_st * (int64_t)(it <= n_valid));
-    }
-    // ---- C tile -> LDS [kTM][256] bf16, 512-B rows, 16-B chunk c of row r at c ^ sw(r), sw(r) = 2 ((r >> 2) & 3):
-    // element (row, col) = (wm kWM + 16 i + 4 fg + r, wn 128 + 16 j + fr)
-    int ez = 0;
-    asm volatile("" : "+v"(ez));
-    unsigned short* const ct = reinterpret_cast<unsigned short*>(smem) + ez;
-    static_for<kFI * 8>([&](auto NC) __attribute__((always_inline)) {
-      constexpr int n = decltype(NC)::value, i = n / 8, j = n % 8;
-      float av[4];  // accumulator (i, j): four per asm statement (hipcc pads each statement's outputs by one state)
-      asm volatile("v_accvgpr_read_b32 %0, a[%4]\n\tv_accvgpr_read_b32 %1, a[%4+1]\n\tv_accvgpr_read_b32 %2, a[%4+2]\n\t"
-                   "v_accvgpr_read_b32 %3, a[%4+3]"
-                   : "=v"(av[0]), "=v"(av[1]), "=v"(av[2]), "=v"(av[3]) : "i"(4 * n));
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-      const int row = wm * kWM + 16 * i + 4 * fg + r;
-      const int col = wn * 128 + 16 * j + fr;
-      const float a = av[r];
-      unsigned short o;
-      if constexpr (kEpi == CP25_EPI_GELU) {
-        const unsigned short u = f2bf(a);
-        const int ti = gelu_tab_index(u);
-        o = reinterpret_cast<const unsigned short*>(smem + kLdsMain)[ti < 0 ? 0 : ti];
-        if (__builtin_expect(__any(ti < 0), 0)) {
-          const unsigned short gs = f2bf(gelu_exact(bf2f(u)));
-          o = ti < 0 ? gs : o;
-        }
-      } else {
-        o = f2bf(rbf(a));
-      }
-      ct[row * 256 + (((col >> 3) ^ (2 * ((row >> 2) & 3))) << 3) + (col & 7)] = o;
-      }
-    });
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    // thread t: rows r0 + 8 it, chunk ch (sw(row) = 2 ((r0 >> 2) & 1) ^ ... per row: row >> 2 = (r0 >> 2) + 2 it)
-    u32x4 cv[kRows];
-#pragma unroll
-    for (int it = 0; it < kRows; ++it) {
-      const int row = r0 + 8 * it;
-      cv[it] = *reinterpret_cast<const u32x4*>(ct + row * 256 + ((ch ^ (2 * ((row >> 2) & 3))) << 3));
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // the LDS is free
-    // CP25_EPI_RES: the gate chunks (one row per frame, L2-resident), requested before the next tile's DMA so the wait
-    // for them and the x chunks leaves that DMA in flight (the VM counter retires in order)
-    u32x4 gres[kEpi == CP25_EPI_RES ? kRows : 1];
-    if constexpr (kEpi == CP25_EPI_RES) {
-      const int row_a = min(m0 + r0, M - 1), tok_a = row_a / re.B, b = row_a % re.B, dtok = 8 / re.B;
-      const int n_valid = (M - 1 - row_a) / 8;
-      const unsigned short* gp = re.gate + b * re.g_sb + n0 + ch * 8;
-      int64_t fr_ = (re.tok0 + tok_a) / re.hw, rem = (re.tok0 + tok_a) % re.hw;
-#pragma unroll
-      for (int it = 0; it < kRows; ++it) {
-        gres[it] = *reinterpret_cast<const u32x4*>(gp + fr_ * re.g_st * (int64_t)(it <= n_valid));
-        rem += dtok;
-        const bool wrap = rem >= re.hw;
-        rem -= wrap ? re.hw : 0;
-        fr_ += wrap ? 1 : 0;
-      }
-    }
-    if constexpr (kEpi == CP25_EPI_QKV) {
-      if (n0 >= re.n_lo && n0 < re.n_hi) {  // a k tile: RMSNorm + RoPE of its two heads per row
-        const int li = ch & 15, dlo = (li & 7) * 8;
-        const float sgn = li < 8 ? -1.f : 1.f;
-        const bool rope = re.rcos != nullptr;
-        const int tok_lo = m0 / re.B;
-        constexpr int kTabBytes = kTM * 256;  // per table: up to kTM tokens x 64 fp32
-        if (rope) {
-          const int ntok = min(M - 1, m0 + kTM - 1) / re.B - tok_lo + 1;
-          const int nbytes = ntok * 256;
-          const __amdgpu_buffer_rsrc_t c_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-              (void*)(re.rcos + (int64_t)tok_lo * 64), (short)0, nbytes, 0x00020000);
-          const __amdgpu_buffer_rsrc_t s_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-              (void*)(re.rsin + (int64_t)tok_lo * 64), (short)0, nbytes, 0x00020000);
-          for (int kb = wave; kb * 1024 < nbytes; kb += k4wThreads / 64) {
-            dma16(c_rsrc, (lds_void_ptr)(smem + kb * 1024), kb * 1024 + 16 * lane, 0);
-            dma16(s_rsrc, (lds_void_ptr)(smem + kTabBytes + kb * 1024), kb * 1024 + 16 * lane, 0);
-          }
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __builtin_amdgcn_s_barrier();
-        }
-        const float* const tcos = reinterpret_cast<const float*>(smem);
-        const float* const tsin = reinterpret_cast<const float*>(smem + kTabBytes);
-#pragma unroll
-        for (int it = 0; it < kRows; ++it) {
-          float v[8];
-#pragma unroll
-          for (int w2 = 0; w2 < 4; ++w2) {
-            v[2 * w2] = bf2f((unsigned short)(cv[it][w2] & 0xffffu));
-            v[2 * w2 + 1] = bf2f((unsigned short)(cv[it][w2] >> 16));
-          }
-          float ss = hn_sumsq8(v);
-#pragma unroll
-          for (int m = 8; m >= 1; m >>= 1) ss += __shfl_xor(ss, m, 16);
-          const float rstd = hn_rstd(ss, re.n_eps);
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            v[e] = hn_norm(v[e], rstd, bf2f((unsigned short)(nwv[e >> 1] >> (16 * (e & 1)))));
-          if (rope) {
-            const int tl = min(m0 + r0 + 8 * it, M - 1) / re.B - tok_lo;
-            const f32x4 c0 = *reinterpret_cast<const f32x4*>(tcos + tl * 64 + dlo);
-            const f32x4 c1 = *reinterpret_cast<const f32x4*>(tcos + tl * 64 + dlo + 4);
-            const f32x4 s0 = *reinterpret_cast<const f32x4*>(tsin + tl * 64 + dlo);
-            const f32x4 s1 = *reinterpret_cast<const f32x4*>(tsin + tl * 64 + dlo + 4);
-            float partner[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) partner[e] = __shfl_xor(v[e], 8, 16);
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-              v[e] = hn_rope(v[e], partner[e], sgn, e < 4 ? c0[e & 3] : c1[e & 3], e < 4 ? s0[e & 3] : s1[e & 3]);
-          }
-          u32x4 o;
-#pragma unroll
-          for (int w2 = 0; w2 < 4; ++w2)
-            o[w2] = (unsigned)f2bf(v[2 * w2] * re.n_scale) | ((unsigned)f2bf(v[2 * w2 + 1] * re.n_scale) << 16);
-          cv[it] = o;
-        }
-        if (rope) {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_s_barrier();
-        }
-      }
-    }
-    const int m0c = m0, n0c = n0;  // this tile's (the loop variables move to the next tile below)
-    const bool full = m0c + kTM <= M;
-    if (has_next) {
-      tile = next;
-      tile_mn(tile, m0, n0);
-      set_tile(m0, n0);
-      dma_ktile(0, 0);
-      dma_ktile(1, 1);
-    }
-    __builtin_amdgcn_sched_barrier(0);  // the DMAs are queued ahead of the stores (the counts rely on it)
-    if constexpr (kEpi == CP25_EPI_HNORM) {
-#pragma unroll
-      for (int it = 0; it < kRows; ++it) {
-        float v[8];
-#pragma unroll
-        for (int w2 = 0; w2 < 4; ++w2) {
-          v[2 * w2] = bf2f((unsigned short)(cv[it][w2] & 0xffffu));
-          v[2 * w2 + 1] = bf2f((unsigned short)(cv[it][w2] >> 16));
-        }
-        float ss = hn_sumsq8(v);
-#pragma unroll
-        for (int m = 8; m >= 1; m >>= 1) ss += __shfl_xor(ss, m, 16);
-        const float rstd = hn_rstd(ss, re.n_eps);
-        u32x4 o;
-#pragma unroll
-        for (int w2 = 0; w2 < 4; ++w2) {
-          const float lo = hn_norm(v[2 * w2], rstd, bf2f((unsigned short)(nwv[w2] & 0xffffu)));
-          const float hi = hn_norm(v[2 * w2 + 1], rstd, bf2f((unsigned short)(nwv[w2] >> 16)));
-          o[w2] = (unsigned)f2bf(lo * re.n_scale) | ((unsigned)f2bf(hi * re.n_scale) << 16);
-        }
-        cv[it] = o;
-      }
-    }
-    if constexpr (kEpi == CP25_EPI_RES) {
-      // the x and gate chunks (older than the next tile's DMA): the DMA pieces may stay in flight
-      if (has_next)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * kPieces) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int it = 0; it < kRows; ++it) cv[it] = res8(cv[it], xres[it], gres[it]);
-    }
-    unsigned short* crow = C + (int64_t)(m0c + r0) * ldc + n0c + ch * 8;
-    const int rows_left = M - (m0c + r0);
-    if (full) {
-#pragma unroll
-      for (int it = 0; it < kRows; ++it) *reinterpret_cast<u32x4*>(crow + (int64_t)it * 8 * ldc) = cv[it];
-    } else {
-#pragma unroll
-      for (int it = 0; it < kRows; ++it)
-        if (it * 8 < rows_left) *reinterpret_cast<u32x4*>(crow + (int64_t)it * 8 * ldc) = cv[it];
-    }
-    if (!has_next) return;
-    // retire the next tile's K-tile 0: K-tile 1 (kPieces) and this tile's stores (kRows, when all issued) may stay
-    stores_pending = full;
-    if (stores_pending)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kPieces + kRows) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kPieces) : "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-}
 }  // namespace
-
-// bf16 GEMM kernel form (cp25_gemm_select): 0 = gemm_nt_8ph (8 waves of 128 x 64), 1 = gemm_nt_4w (4 waves of
-// 128 x 128). Set only through cp25_gemm_select (never per launch, never from the environment).
-static int g_gemm_form = 0;
-
-extern "C" int cp25_gemm_select(int form) {
-  if (form != 0 && form != 1) return CP25_ERR_INVAL;
-  const int prev = g_gemm_form;
-  g_gemm_form = form;
-  return prev;
-}
-
-template <int kTM>
-static void launch_4w(int epilogue, dim3 grid, hipStream_t stream, const unsigned short* A, int64_t lda,
-                      const unsigned short* Wp, int64_t ldw, unsigned short* Cp, int64_t ldc, int M, int N, int K,
-                      const ResEpi& re) {
-  const dim3 block(k4wThreads);
-  switch (epilogue) {
-    case CP25_EPI_GELU:
-      hipLaunchKernelGGL((gemm_nt_4w<CP25_EPI_GELU, kTM>), grid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re);
-      break;
-    case CP25_EPI_RES:
-      hipLaunchKernelGGL((gemm_nt_4w<CP25_EPI_RES, kTM>), grid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re);
-      break;
-    case CP25_EPI_HNORM:
-      hipLaunchKernelGGL((gemm_nt_4w<CP25_EPI_HNORM, kTM>), grid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re);
-      break;
-    case CP25_EPI_QKV:
-      hipLaunchKernelGGL((gemm_nt_4w<CP25_EPI_QKV, kTM>), grid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re);
-      break;
-    default:
-      hipLaunchKernelGGL((gemm_nt_4w<CP25_EPI_NONE, kTM>), grid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re);
-  }
-}
 
 static int gemm_launch(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int M, int N,
                        int K, int epilogue, const ResEpi& re, hipStream_t stream) {
@@ -1225,11 +760,7 @@ static int gemm_launch(const void* a, int64_t lda, const void* w, int64_t ldw, v
     return CP25_ERR_LAUNCH;
   const int cus = n_cu[dev] >= 8 ? n_cu[dev] & ~7 : n_cu[dev];
   const dim3 pgrid((unsigned)std::min<int64_t>(nwg, cus));
-  // (the 4w gated-residual and QKV epilogues are not enabled yet: register pressure)
-  const bool epi_4w = epilogue == CP25_EPI_NONE || epilogue == CP25_EPI_GELU || epilogue == CP25_EPI_HNORM;
-  if (g_gemm_form == 1 && (K / kBK) % 2 == 0 && epi_4w) {
-    launch_4w<256>(epilogue, pgrid, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re);
-  } else if ((K / kBK) % 2 != 0) {
+  if ((K / kBK) % 2 != 0) {
     switch (epilogue) {
       case CP25_EPI_GELU:
         hipLaunchKernelGGL(gemm_nt_kernel<CP25_EPI_GELU>, grid, block, 0, stream, A, lda, Wp, ldw, Cp, ldc, M, N, K, re);

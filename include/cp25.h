@@ -279,12 +279,6 @@ int64_t cp25_gemm_f32_workspace_floats(int M, int N, int K, int batch);
 int cp25_gemm_epi(const void* a, int64_t lda, const void* w, int64_t ldw, void* c, int64_t ldc, int M, int N, int K,
                   int epilogue, hipStream_t stream);
 
-/* Kernel form of the bf16 block GEMMs (cp25_gemm_epi / _res / _hnorm / _qkv): 0 gemm_nt_8ph (8 waves of 128 x 64 per
- * 256 x 256 tile, two waves per SIMD), 1 gemm_nt_4w (4 waves of 128 x 128, one wave per SIMD; the gated residual
- * needs 8 % B == 0 and hw >= 8 / B). Both accumulate every output in the same order: bit-identical. Returns the
- * previous form, or CP25_ERR_INVAL for another value. No reference counterpart (a kernel choice, not an op). */
-int cp25_gemm_select(int form);
-
 /* cp25_gemm_epi with the per-head q RMSNorm as the epilogue (CP25_EPI_HNORM): every 128-column head of each output row
  * of bf16(A W^T) normalised over its 128 values (norm_weight [128] bf16, eps) and multiplied by out_scale, with the
  * partial sums, butterfly and roundings of cp25_head_rmsnorm_rope (no RoPE): bit-identical to cp25_gemm_epi followed

@@ -120,16 +120,16 @@ def test_sampler_matches_oracle(device, guidance, tol):
     assert err <= tol, err
 
 
-def test_sampler_small_frames_library_residual(device):
+def test_sampler_small_frames_unfused_residual(device):
     """A 4 x 6 latent (hw = 2 x 3 = 6 tokens per frame): the fused gated-residual GEMM needs at least 16 / B tokens per
     frame (gemm_res_supported: 16 at the CFG-shared block 0's B = 1, 8 at B = 2), so every residual projection takes
-    the library GEMM with the residual in cp25_ln_mod / the final layer instead of raising. Same oracle bound as the
+    the plain own GEMM with the residual in cp25_ln_mod / the final layer instead of raising. Same oracle bound as the
     16 x 16 case."""
     from cosmos_predict2 import _native as N
 
     assert not N.gemm_res_supported(512, 512, 1, 6) and not N.gemm_res_supported(512, 512, 2, 6)
     err = _sampler_case(device, 0.0, T=3, H=4, W=6)
-    print(f"sampler vs oracle at a 4 x 6 latent (library residual path): {err:.3e}")
+    print(f"sampler vs oracle at a 4 x 6 latent (unfused residual path): {err:.3e}")
     assert err <= 1e-2, err
 
 
@@ -244,9 +244,8 @@ def test_config1_shape_2b_width_sampler_matches_oracle(device):
 def test_shared_cfg_block0(device, two_b):
     """The CFG pair shares x, t and the action, so block 0's self-attention sub-layer, its residual and the
     cross-attention query run once (MinimalV1LVGDiT._blocks, shared_batch). Tiny widths: the same trajectory
-    bit for bit as with every entry computing them (share_cfg_block0 = False). 2B widths: the library GEMMs
-    pick other kernels for n rows than for 2n (accumulation order, bf16 rounding of some outputs), so the
-    check is against the oracle: the shared path is as close to it as the per-entry path (guidance 0, where
+    bit for bit as with every entry computing them (share_cfg_block0 = False). 2B widths: checked against the oracle
+    (written when library GEMMs picked other kernels for n rows than for 2n): the shared path is as close to it as the per-entry path (guidance 0, where
     the CFG difference is not amplified)."""
     from cosmos_predict2.net_config import DIT_2B
 

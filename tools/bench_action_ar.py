@@ -36,7 +36,10 @@ def main():
     n_chunks = -(-(a.frames - 1) // a.chunk_size)
     inf = ActionConditionedInference(device=dev, state_t=1 + a.chunk_size // 4, linear_precision=a.linear_precision,
                                      attention_precision=a.attention_precision)
-    inf.pipe.model.net.block_gemm = a.block_gemm
+    if a.block_gemm == "lib":
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from library_gemm_net import use_library_gemms
+        use_library_gemms(inf.pipe.model.net)
     adim = inf.pipe.model.net.cfg.action_dim
     rng = np.random.RandomState(0)
     img = rng.randint(0, 256, size=(h, w, 3), dtype=np.uint8)

@@ -97,6 +97,11 @@ def main():
                     help="with --bounded --prescaled: q stays the raw projection and the kernel applies the q RMSNorm "
                          "+ RoPE + prescale itself (cp25_attn_fwd_prescaled_qnorm, the DiT's default since round 4)")
     ap.add_argument("--lib", default="", help="lab build of libcp25.so to load instead of the in-tree one")
+    ap.add_argument("--self-form", type=int, default=-1,
+                    help="w64 lab library (tools/lab/w64/build_lab.sh, with --lib): prescaled self-attention form, 0 attn_fwd_m16, 1 w64 in the zero / fixed modes, 2 w64 in all (cp25_attn_self_select)")
+    ap.add_argument("--ab", type=int, default=0,
+                    help="A/B: after the timing, N more rounds alternating attn_fwd_m16 / attn_fwd_w64 launches "
+                         "(iters each), reported as ms lists per form")
     ap.add_argument("--probe", type=int, default=-1,
                     help="with a -DCP25_ATTN_PROBE lab build: after the timing, one more launch records s_memtime "
                          "stamps of tiles probe .. probe + 31 in the first --probe-wg workgroups (probe_report)")
@@ -108,6 +113,8 @@ def main():
     a = ap.parse_args()
     if a.lib:
         N._LIB_PATH = a.lib
+    if a.self_form >= 0:
+        N.attn_self_select(a.self_form)
     dev = torch.device("cuda:0")
     Lk = a.Lk or a.L
     g = torch.Generator(device=dev).manual_seed(0)
@@ -179,6 +186,21 @@ def main():
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
     flop = 4.0 * a.B * a.H * a.L * Lk * 128
+    ab = None
+    if a.ab > 0:
+        ab = {"m16": [], "w64": []}
+        prev = N.attn_self_select(0)
+        for _ in range(a.ab):
+            for form, key in ((0, "m16"), (1, "w64")):
+                N.attn_self_select(form)
+                N.attn_fwd(q, k, v, out=o, n_split=ns, norm_bounds=nb, **pre)
+                e0.record(st)
+                for _ in range(a.iters):
+                    N.attn_fwd(q, k, v, out=o, n_split=ns, norm_bounds=nb, **pre)
+                e1.record(st)
+                torch.cuda.synchronize()
+                ab[key].append(round(e0.elapsed_time(e1) / a.iters, 3))
+        N.attn_self_select(prev)
     probe = None
     if a.probe >= 0:
         import ctypes
@@ -197,7 +219,7 @@ def main():
         probe = probe_report(pb[:n_t].reshape(a.probe_wg, 8, 32, 4), pb[n_t:].reshape(a.probe_wg, 8, 8))
     print(json.dumps({"kernel": "attn_fwd", "B": a.B, "H": a.H, "Lq": a.L, "Lk": Lk, "fused": a.fused,
                       "zeros": a.zeros, "bounded": a.bounded, "prescaled": a.prescaled, "fp8qk": a.fp8qk, "fp8pv": a.fp8pv, "qnorm": a.qnorm, "force_online": a.force_online, "normed": a.normed or a.bounded, "wrange": a.wrange, "split": ns or N.attn_plan(a.B, a.H, a.L, Lk), "iters": a.iters, "lib": os.path.basename(a.lib) or "libcp25.so", "ms": ms,
-                      "tflops": flop / ms / 1e9, "check_rel_l2": check, **({"probe": probe} if probe else {})}))
+                      "tflops": flop / ms / 1e9, "check_rel_l2": check, "kernel_name": N.attn_kernel_name(Lk, norm_bounds=nb, prescaled=a.prescaled), **({"probe": probe} if probe else {}), **({"ab_ms": ab} if ab else {})}))
 
 
 if __name__ == "__main__":

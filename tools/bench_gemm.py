@@ -40,8 +40,6 @@ def main():
     ap.add_argument("--shapes", default="qkv,proj,mlp1,mlp2")
     ap.add_argument("--plain", action="store_true")
     ap.add_argument("--lib", default="")
-    ap.add_argument("--forms", default="", help="e.g. 0,1: time the own GEMM in each cp25_gemm_select form "
-                    "(own_ms_form<f>; --plain only)")
     a = ap.parse_args()
     if a.lib:
         N._LIB_PATH = a.lib
@@ -70,18 +68,9 @@ def main():
                        scaled_mm_tflops=flop / min(res["lib"]) / 1e9, own_tflops=flop / min(res["own"]) / 1e9)
             print(json.dumps(rec), flush=True)
             continue
-        forms = [int(f) for f in a.forms.split(",")] if a.forms else []
-        for f in forms:
-            res[f"own_form{f}"] = []
         for _ in range(a.rounds):
             res["lib"].append(timed(lambda: torch.matmul(x, w.t(), out=out)))
             res["own"].append(timed(lambda: N.gemm_epi(x, w, out=out)))
-            for f in forms:
-                prev = N.gemm_select(f)
-                res[f"own_form{f}"].append(timed(lambda: N.gemm_epi(x, w, out=out)))
-                N.gemm_select(prev)
-        for f in forms:
-            rec[f"own_ms_form{f}"] = res[f"own_form{f}"]
         rec.update(kind="bf16", hipblaslt_ms=res["lib"], own_ms=res["own"],
                    hipblaslt_tflops=flop / min(res["lib"]) / 1e9, own_tflops=flop / min(res["own"]) / 1e9)
         if a.plain:
