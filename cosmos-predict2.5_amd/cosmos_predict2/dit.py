@@ -475,6 +475,10 @@ class MinimalV1LVGDiT:
         self.w_ada2 = torch.stack([p[f"blocks.{i}.adaln_modulation_{m}.2.weight"]
                                    for i in range(cfg.num_blocks) for m in ("self_attn", "cross_attn", "mlp")], 0).float()
         self.w_final = p["final_layer.linear.weight"].float()
+        if not cfg.use_wan_fp32_strategy:  # the bf16 final linear on the own GEMM: N padded with zero rows to 256
+            wf = p["final_layer.linear.weight"]
+            self.w_final_bf16 = torch.zeros(((wf.shape[0] + 255) // 256 * 256, D), dtype=BF16, device=dev)
+            self.w_final_bf16[: wf.shape[0]] = wf
         # fp32 copies of the conditioning weights (the reference runs these layers under fp32 autocast)
         self.w_t1 = p["t_embedder.1.linear_1.weight"].float()
         self.w_t2 = p["t_embedder.1.linear_2.weight"].float()
@@ -644,20 +648,42 @@ class MinimalV1LVGDiT:
         return e_d, e_3d
 
     @torch.no_grad()
-    def time_modulation(self, t_B_T: torch.Tensor, action: Optional[torch.Tensor] = None):
-        """t (already * timestep_scale) [B, T] fp32 -> (block mods bf16 [nb, 3, B, T, 3D],
-        final shift/scale fp32 [B, T, D] each). fp32 math (use_wan_fp32_strategy). Action nets add
-        the action embeddings to the embedding and the AdaLN-LoRA term before the norm
-        (action_conditioned_minimal_v1_lvg_dit.py:298-305)."""
-        cfg = self.cfg
-        p = self.sd
-        D = cfg.model_channels
+    def scale_timesteps(self, t: torch.Tensor) -> torch.Tensor:
+        """The net's `timesteps_B_T * self.timestep_scale` (minimal_v1_lvg_dit.py:49, multiview_dit.py:535) of the
+        sampler's fp32 timesteps, as fp32 values for forward_tokens. use_wan_fp32_strategy nets: in fp32. The others
+        (the multi-view nets, predict2_multiview/configs/vid2vid/defaults/net.py:52,105) take t in the net's dtype:
+        bf16(bf16(t) * scale). The reference's rectified-flow denoise hands these nets fp32 timesteps
+        (video2world_model_rectified_flow.py:113-127), which the bf16 t-embedder cannot take without the fp32
+        autocast the flag turns off (TimestepEmbedding.linear_1, minimal_v4_dit.py:776, would raise on an fp32 input
+        against its bf16 weight); its EDM denoise casts them to the net dtype exactly when the flag is off
+        (video2world_model.py:231-236), and that is the cast restated here."""
+        t = t.to(self.device).float()
+        if self.cfg.use_wan_fp32_strategy:
+            return t * self.cfg.timestep_scale
+        return (t.to(BF16) * self.cfg.timestep_scale).float()
+
+    def _sincos(self, t_B_T: torch.Tensor) -> torch.Tensor:
+        """Timesteps (minimal_v4_dit.py:727-747): [cos | sin] of t * 10000^(-i / half) in fp32 -> [B, T, D] fp32."""
+        D = self.cfg.model_channels
         B, T = t_B_T.shape
         half = D // 2
         expo = -math.log(10000) * torch.arange(half, dtype=F32, device=self.device)
         expo = expo / (half - 0.0)
         arg = t_B_T.flatten().float()[:, None] * torch.exp(expo)[None, :]
-        sincos = torch.cat([torch.cos(arg), torch.sin(arg)], dim=-1).view(B, T, D)
+        return torch.cat([torch.cos(arg), torch.sin(arg)], dim=-1).view(B, T, D)
+
+    def time_modulation(self, t_B_T: torch.Tensor, action: Optional[torch.Tensor] = None):
+        """t (scale_timesteps) [B, T] fp32 -> (block mods bf16 [nb, 3, B, T, 3D], final shift / scale [B, T, D] each:
+        fp32 under use_wan_fp32_strategy, else bf16). fp32 math (use_wan_fp32_strategy), else _time_modulation_bf16.
+        Action nets add the action embeddings to the embedding and the AdaLN-LoRA term before the norm
+        (action_conditioned_minimal_v1_lvg_dit.py:298-305)."""
+        cfg = self.cfg
+        if not cfg.use_wan_fp32_strategy:
+            return self._time_modulation_bf16(t_B_T, action)
+        p = self.sd
+        D = cfg.model_channels
+        B, T = t_B_T.shape
+        sincos = self._sincos(t_B_T)
         # every fp32 linear below on cp25_gemm_f32 (fp32 MFMA): TimestepEmbedding (minimal_v4_dit.py:727-788)
         h = N.gemm_f32(sincos.view(B * T, D), self.w_t1, act=N.ACT_SILU)
         lora = N.gemm_f32(h, self.w_t2).view(B, T, 3 * D)
@@ -683,6 +709,42 @@ class MinimalV1LVGDiT:
         f1 = N.gemm_f32(se, self.w_f1)
         f2 = N.gemm_f32(f1, self.w_f2, add=lora2[:, : 2 * D]).view(B, T, 2 * D)
         shift_f, scale_f = f2.chunk(2, dim=-1)
+        return mods, shift_f, scale_f
+
+    def _time_modulation_bf16(self, t_B_T: torch.Tensor, action: Optional[torch.Tensor] = None):
+        """time_modulation of a net with use_wan_fp32_strategy=False: the same layers without the fp32 autocast
+        (multiview_dit.py:544-548 / multiview_cross_dit.py:823-827, minimal_v4_dit.py:1136-1154 AdaLN, :974-995 final
+        layer), i.e. in the net's bf16. Every linear is a bf16 GEMM (bf16 operands, fp32 accumulation, one bf16
+        rounding: cp25_gemm_f32 on the bf16 values, rounded), every elementwise op one bf16 torch op: the sinusoid
+        rounded to bf16, SiLU on the rounded linear_1 output, TE RMSNorm (fp32 math, one rounding), the AdaLN-LoRA
+        sum `modulation(emb) + lora` of two bf16 tensors. Returns bf16 shift / scale for the final layer."""
+        cfg = self.cfg
+        D = cfg.model_channels
+        B, T = t_B_T.shape
+
+        def lin(x, w, **kw):  # bf16 nn.Linear (no bias) of bf16 x on the fp32 MFMA GEMM, one rounding
+            return N.gemm_f32(x.float(), w, **kw).to(BF16)
+
+        sincos = self._sincos(t_B_T).to(BF16).view(B * T, D)
+        h = F.silu(lin(sincos, self.w_t1))
+        lora = lin(h, self.w_t2)  # [BT, 3D]
+        if cfg.action_dim:
+            if action is None:
+                raise ValueError("this action-conditioned net needs `action`")
+            e_d, e_3d = self.action_embedding(action, B, T)
+            sincos = sincos + e_d.reshape(B * T, D)
+            lora = lora + e_3d.reshape(B * T, 3 * D)
+        elif action is not None:
+            raise ValueError("`action` given to a net without action embedders")
+        xf = sincos.float()
+        emb = ((xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-6)) * self.sd["t_embedding_norm.weight"].float())
+        se = F.silu(emb.to(BF16))  # [BT, D] bf16
+        nb3 = 3 * cfg.num_blocks
+        a1 = lin(se, self.w_ada1).view(B * T, nb3, -1).transpose(0, 1)  # [nb3, BT, A]
+        a2 = lin(a1, self.w_ada2)  # [nb3, BT, 3D]
+        mods = (a2 + lora[None]).view(cfg.num_blocks, 3, B, T, 3 * D)
+        f2 = lin(lin(se, self.w_f1), self.w_f2) + lora[:, : 2 * D]
+        shift_f, scale_f = f2.view(B, T, 2 * D).chunk(2, dim=-1)
         return mods, shift_f, scale_f
 
     # ---------------------------------------------------------------- hot path
@@ -821,12 +883,14 @@ class MinimalV1LVGDiT:
 
     def _view_modulation(self, mods: torch.Tensor, geo: Geometry, view_indices: Optional[torch.Tensor]) -> torch.Tensor:
         """Cross-view nets' AdaLN view embedding (multiview_cross_dit.py:807-813, 355-404): adaln_view_proj(
-        adaln_view_embedder(view id)) [V, 9D] (fp32, cp25_gemm_f32 with the bias as addend) in the chunk order
+        adaln_view_embedder(view id)) [V, 9D] (cp25_gemm_f32 with the bias as addend, rounded to bf16: the fp32-autocast
+        linear, or with use_wan_fp32_strategy=False the bf16 linear, whose bf16 operands make the same sums) in the chunk order
         (shift, scale, gate) x (self-attn, cross-attn, mlp), rounded to bf16 and added to the bf16 modulation of every
         frame of the view (one bf16 rounding, the reference's `m + view_m.type_as(x)`)."""
         cfg, D, V = self.cfg, self.cfg.model_channels, geo.n_views
         ids = self._view_ids(geo, view_indices)
         e = self.sd["adaln_view_embedder.weight"][ids].float()
+        # (the same sums either way: bf16 e, w and bias, fp32 accumulation with the bias, one rounding to bf16)
         vp = N.gemm_f32(e, self.w_view_proj, add=self.b_view_proj).to(BF16).view(V, 3, 3 * D)
         per_frame = vp.repeat_interleave(geo.T_view, dim=0)  # [T, 3, 3D]: frame t belongs to view t // T_view
         if mods.shape[3] != per_frame.shape[0]:
@@ -1048,6 +1112,13 @@ class MinimalV1LVGDiT:
             if cp is None or cp_size == 1:
                 yield i
         # ---- final layer (fp32 autocast): x + g*y -> LN -> modulate -> Linear(D -> 64)
+        if not cfg.use_wan_fp32_strategy:
+            # FinalLayer without the fp32 autocast (minimal_v4_dit.py:974-995): LayerNorm, * (1 + scale), + shift as
+            # bf16 ops (cp25_ln_mod's arithmetic, with the last residual) and a bf16 linear on the own GEMM
+            x_new = torch.empty((n, B, D), dtype=BF16, device=self.device) if y is not None else None
+            h = N.ln_mod(x, shift_f, scale_f, x_st=B * D, x_sb=D, y=y, gate=gate_prev, x_out=x_new, **common)
+            out = N.gemm_epi(h.view(n * B, D), self.w_final_bf16)[:, : self.w_final.shape[0]].float()
+            return out.view(n, B, -1)
         xf = N.final_ln_mod(x, shift_f, scale_f, y=y, gate=gate_prev, **common)
         out = N.gemm_f32(xf.view(n * B, D), self.w_final, split_k=False)  # rows independent of the shard size
         return out.view(n, B, -1)
@@ -1150,7 +1221,7 @@ class MinimalV1LVGDiT:
         ctx = self.prepare_context(crossattn_emb)
         if timesteps_B_T.ndim == 1:
             timesteps_B_T = timesteps_B_T.unsqueeze(1)
-        t = timesteps_B_T.to(self.device).float() * cfg.timestep_scale
+        t = self.scale_timesteps(timesteps_B_T)
         if t.shape[1] == 1 and T > 1:
             t = t.expand(B, T).contiguous()
         out = self.forward_tokens(rows.contiguous(), t, ctx, geo, action=action,

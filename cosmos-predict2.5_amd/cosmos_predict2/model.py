@@ -284,7 +284,7 @@ class SamplingRun:
         t = self.timesteps[self.i]
         rows = N.patchify(self.x, self.gtp, self.frame_mask, None, tok0=geo.tok0, hw=geo.hw, ld=128)
         tf = m._frame_timesteps(t, self.frame_mask)  # [T]
-        t_B_T = (tf[None, :] * m.net_cfg.timestep_scale).expand(2, geo.T).contiguous()
+        t_B_T = m.net.scale_timesteps(tf[None, :]).expand(2, geo.T).contiguous()
         if self.net_fn is None:
             # one t row expanded over the CFG pair, one action: the entries differ only in the text context
             shared = self.action is None or self.action.shape[0] == 1

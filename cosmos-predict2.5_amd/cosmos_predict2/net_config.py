@@ -124,20 +124,20 @@ SAMPLER_ACTION = SamplerConfig(state_t=4, resolution="256")
 # net COSMOS_V1_2B_MULTIVIEW_NET, defaults/net.py:26-63): 7 camera embeddings of 7 channels, state_t 8 per
 # view (29 frames), RoPE h/w 3.0, t 8/24, fps modulation off; CFG uncond + g (cond - uncond)
 # (multiview_vid2vid_model_rectified_flow.py:381); the first n latent frames of every view are conditioned.
+# Both multi-view nets set use_wan_fp32_strategy=False (defaults/net.py:52, 105): the t-embedding, AdaLN and final
+# layer run in the net's bf16 (MinimalV1LVGDiT._time_modulation_bf16, scale_timesteps).
 DIT_2B_MULTIVIEW = DIT_2B.replace(n_cameras_emb=7, view_condition_dim=7, state_t=8,
-                                  rope_t_extrapolation_ratio=8.0 / 24.0)
+                                  rope_t_extrapolation_ratio=8.0 / 24.0, use_wan_fp32_strategy=False)
 SAMPLER_MULTIVIEW = SamplerConfig(state_t=8, cfg_mode="text2world", resolution="720")
 # cross-view multi-view net (COSMOS_V1_2B_MULTIVIEW_CROSSVIEW_NET, predict2_multiview/configs/vid2vid/defaults/net.py:
 # 76-107: adaln view embedding, no view-embedding input channels, cross-view attention) with the crossview experiment's
 # neighbour map (experiment/buttercup/buttercup2p5_rectified_flow.py:387-399) in the view ids of
 # predict2_multiview/scripts/inference.py:61-69 (front_wide 0, cross_right 1, rear_right 2, rear_tele 3, rear_left 4,
-# cross_left 5, front_tele 6); state_t and RoPE as the multiview experiment above. The registered config sets
-# use_wan_fp32_strategy=False, whose conditioning precision is the caller's autocast; this build runs the conditioning
-# in fp32 (the fp32 strategy) for every net.
+# cross_left 5, front_tele 6); state_t, RoPE and use_wan_fp32_strategy=False as the multiview net above.
 CROSS_VIEW_MAP_7 = ((5, 1, 6), (0, 2), (1, 3), (4, 2), (5, 3), (0, 4), (0,))
 DIT_2B_MULTIVIEW_CROSSVIEW = DIT_2B.replace(n_cameras_emb=7, view_condition_dim=0, state_t=8,
                                             rope_t_extrapolation_ratio=8.0 / 24.0, adaln_view_embedding=True,
-                                            cross_view_attn_map=CROSS_VIEW_MAP_7)
+                                            cross_view_attn_map=CROSS_VIEW_MAP_7, use_wan_fp32_strategy=False)
 
 # model name (cosmos_predict2/config.py ModelKey.name) -> (net, sampler)
 MODELS = {

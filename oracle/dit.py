@@ -5,6 +5,12 @@ net weights and float buffers in bf16 (utils/model_loader.py:88-90 + on_train_st
 for the block body, fp32 autocast for the t-embedding, AdaLN modulation and final layer
 (use_wan_fp32_strategy, minimal_v4_dit.py:974-995, 1136-1154, 1615-1619), q/k upcast to fp32 for
 RoPE (:415-419) and recast to bf16 by attention() (networks/attention.py:107-109).
+Nets with use_wan_fp32_strategy=False (the multi-view nets, predict2_multiview/configs/vid2vid/defaults/net.py:52,
+105) run those layers without the autocast, in the net's bf16 (multiview_dit.py:544-548, multiview_cross_dit.py:334,
+823-835), with the timesteps in the net dtype (the cast video2world_model.py:231-236 applies when the flag is off;
+the rectified-flow denoise passes fp32 timesteps, which the bf16 TimestepEmbedding.linear_1 cannot take without the
+autocast, minimal_v4_dit.py:776). Their RoPE skips the fp32 upcast (:415-419), but TE's fused RoPE computes in fp32
+and rounds once to the input dtype, which is where attention() rounds the upcast q / k: the same values either way.
 
 Paths relative to cosmos_predict2/_src/predict2/networks/ unless stated:
   minimal_v1_lvg_dit.py:31-62      condition-mask channel, timestep scale
@@ -192,28 +198,37 @@ def action_embedding(cfg, sd, action: torch.Tensor):
     return e_d, e_3d
 
 
+def cond_dtype(cfg) -> torch.dtype:
+    """dtype of the t-embedding, AdaLN, view projection and final layer: fp32 (the autocast of
+    use_wan_fp32_strategy, and the fp32 truth), else the net's bf16."""
+    return F32 if cfg.get("use_wan_fp32_strategy", True) or act_dtype() == F32 else BF16
+
+
 def timestep_embedding(cfg, sd, t_B_T: torch.Tensor, action: torch.Tensor | None = None):
-    """Timesteps + TimestepEmbedding(adaln-lora) + t_embedding_norm, fp32 (autocast); action nets add
-    the action embeddings before the norm (action_conditioned_minimal_v1_lvg_dit.py:298-305)."""
+    """Timesteps (fp32 sinusoid, returned in t's dtype) + TimestepEmbedding(adaln-lora) + t_embedding_norm in the
+    conditioning dtype (cond_dtype); action nets add the action embeddings before the norm
+    (action_conditioned_minimal_v1_lvg_dit.py:298-305)."""
     D = cfg["model_channels"]
+    cd = cond_dtype(cfg)
     half = D // 2
     expo = -math.log(10000) * torch.arange(half, dtype=F32, device=t_B_T.device) / (half - 0.0)
     emb = t_B_T.flatten().float()[:, None] * torch.exp(expo)[None, :]
-    sincos = torch.cat([torch.cos(emb), torch.sin(emb)], dim=-1).reshape(t_B_T.shape[0], t_B_T.shape[1], D)
-    h = F.silu(_lin(sincos, _w(sd, "t_embedder.1.linear_1.weight").float()))
-    lora = _lin(h, _w(sd, "t_embedder.1.linear_2.weight").float())
+    sincos = torch.cat([torch.cos(emb), torch.sin(emb)], dim=-1).reshape(t_B_T.shape[0], t_B_T.shape[1], D).to(cd)
+    h = F.silu(_lin(sincos, _w(sd, "t_embedder.1.linear_1.weight").to(cd)))
+    lora = _lin(h, _w(sd, "t_embedder.1.linear_2.weight").to(cd))
     if action is not None:
         e_d, e_3d = action_embedding(cfg, sd, action)
-        sincos = sincos + e_d.float()
-        lora = lora + e_3d.float()
+        sincos = sincos + e_d.to(cd)
+        lora = lora + e_3d.to(cd)
     emb_norm = te_rmsnorm(sincos, _w(sd, "t_embedding_norm.weight"))
     return emb_norm, lora
 
 
 def adaln(sd, prefix, emb, lora, n_chunks=3):
+    """SiLU -> Linear(D, A) -> Linear(A, n D), + the AdaLN-LoRA term, in emb's dtype (cond_dtype)."""
     h = F.silu(emb)
-    h = _lin(h, _w(sd, prefix + ".1.weight").float())
-    h = _lin(h, _w(sd, prefix + ".2.weight").float())
+    h = _lin(h, _w(sd, prefix + ".1.weight").to(emb.dtype))
+    h = _lin(h, _w(sd, prefix + ".2.weight").to(emb.dtype))
     return (h + lora[..., : h.shape[-1]]).chunk(n_chunks, dim=-1)
 
 
@@ -326,7 +341,12 @@ def dit_forward(cfg: dict, sd: dict, x_B_C_T_H_W: torch.Tensor, timesteps_B_T: t
     x = x_B_C_T_H_W.to(act_dtype())
     B, C, T, Hl, Wl = x.shape
     x = torch.cat([x, cond_mask_B_1_T_H_W.to(act_dtype())], dim=1)  # minimal_v1_lvg_dit.py:46
-    t = timesteps_B_T * cfg["timestep_scale"]
+    if not cfg.get("use_wan_fp32_strategy", True):
+        # timesteps in the net dtype (module docstring); the fp32 truth takes the same bf16 input values
+        t = timesteps_B_T.to(BF16)
+        t = t * cfg["timestep_scale"] if act_dtype() == BF16 else t.float() * cfg["timestep_scale"]
+    else:
+        t = timesteps_B_T * cfg["timestep_scale"]
     if cfg["concat_padding_mask"]:
         pm = padding_mask_B_1_H_W if padding_mask_B_1_H_W is not None else torch.zeros(B, 1, Hl, Wl, device=x.device)
         pm = F.interpolate(pm.float(), size=(Hl, Wl), mode="nearest").to(act_dtype())
@@ -358,20 +378,22 @@ def dit_forward(cfg: dict, sd: dict, x_B_C_T_H_W: torch.Tensor, timesteps_B_T: t
     emb, lora = timestep_embedding(cfg, sd, t, action)
     view_mod = None
     if cfg.get("adaln_view_embedding"):
-        # adaln_view_proj(adaln_view_embedder(view id)) (multiview_cross_dit.py:807-813; fp32 as the conditioning
-        # strategy of this build) -> 9 chunks, each per frame of its view, cast to the activation dtype
-        e = _w(sd, "adaln_view_embedder.weight")[torch.tensor(view_ids, device=x.device)].float()
-        vp = _lin(e, _w(sd, "adaln_view_proj.weight").float(), _w(sd, "adaln_view_proj.bias").float())
+        # adaln_view_proj(adaln_view_embedder(view id)) (multiview_cross_dit.py:829-835, in cond_dtype) -> 9 chunks,
+        # each per frame of its view, cast to the activation dtype
+        cd = cond_dtype(cfg)
+        e = _w(sd, "adaln_view_embedder.weight")[torch.tensor(view_ids, device=x.device)].to(cd)
+        vp = _lin(e, _w(sd, "adaln_view_proj.weight").to(cd), _w(sd, "adaln_view_proj.bias").to(cd))
         view_mod = vp.to(act_dtype()).view(n_views, 9, -1).repeat_interleave(Tp // n_views, dim=0).transpose(0, 1)
     for i in range(cfg["num_blocks"]):
         x = block_forward(cfg, sd, i, x, emb, lora, ctx, freqs, n_views, view_mod, view_ids)
 
-    # final layer (fp32 autocast)
+    # final layer (fp32 autocast, or bf16 ops without the fp32 strategy)
     D = cfg["model_channels"]
+    cd = cond_dtype(cfg)
     sh, sc = adaln(sd, "final_layer.adaln_modulation", emb, lora[..., : 2 * D], n_chunks=2)
-    xf = F.layer_norm(x.float(), (D,), eps=1e-6)
+    xf = F.layer_norm(x.to(cd), (D,), eps=1e-6)
     xf = xf * (1 + sc[:, :, None, None, :]) + sh[:, :, None, None, :]
-    out = _lin(xf, _w(sd, "final_layer.linear.weight").float())  # [B,Tp,Hp,Wp, p1*p2*pt*C]
+    out = _lin(xf, _w(sd, "final_layer.linear.weight").to(cd))  # [B,Tp,Hp,Wp, p1*p2*pt*C]
     Cout = cfg["out_channels"]
     out = out.reshape(B, Tp, Hp, Wp, ps, ps, pt, Cout).permute(0, 7, 1, 6, 2, 4, 3, 5)
     return out.reshape(B, Cout, Tp * pt, Hp * ps, Wp * ps).float()

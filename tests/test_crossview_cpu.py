@@ -17,17 +17,18 @@ T_VIEW, HP, WP = 2, 4, 8
 MAP = ((1, 2), (0,), (0, 1))
 
 
-def _cfg():
+def _cfg(wan_fp32=False):
     from cosmos_predict2.net_config import tiny_dit
-    return tiny_dit(num_blocks=2, n_cameras_emb=3, state_t=T_VIEW, adaln_view_embedding=True, cross_view_attn_map=MAP)
+    return tiny_dit(num_blocks=2, n_cameras_emb=3, state_t=T_VIEW, adaln_view_embedding=True, cross_view_attn_map=MAP,
+                    use_wan_fp32_strategy=wan_fp32)
 
 
-def _run(view_ids):
+def _run(view_ids, wan_fp32=False):
     import cpu_kernels
     from cosmos_predict2.dit import MinimalV1LVGDiT, init_state_dict
     from oracle import dit as odit
 
-    cfg = _cfg()
+    cfg = _cfg(wan_fp32)
     sd = {"net." + k: v for k, v in init_state_dict(cfg, seed=4, zero_adaln_out=False).items()}
     V = len(view_ids)
     T = V * T_VIEW
@@ -46,10 +47,12 @@ def _run(view_ids):
     return ((out.float() - ref).norm() / ref.norm()).item(), net
 
 
-@pytest.mark.parametrize("view_ids", [[0, 1, 2], [0, 2], [2, 1]])
-def test_crossview_forward_matches_oracle_cpu(view_ids):
-    rel, _ = _run(view_ids)
-    print(f"cross-view net, views {view_ids}: rel-L2 {rel:.3e}")
+@pytest.mark.parametrize("view_ids,wan_fp32", [([0, 1, 2], False), ([0, 2], False), ([2, 1], False),
+                                               ([0, 1, 2], True)])
+def test_crossview_forward_matches_oracle_cpu(view_ids, wan_fp32):
+    """wan_fp32=False is the registered cross-view net's conditioning arithmetic (bf16); True the fp32 strategy."""
+    rel, _ = _run(view_ids, wan_fp32)
+    print(f"cross-view net, views {view_ids}, wan_fp32 {wan_fp32}: rel-L2 {rel:.3e}")
     assert rel <= 1e-2, rel
 
 

@@ -54,12 +54,15 @@ def _case(device, cfg, view_ids, t_view, hp, wp, seed=4):
     return ((out.float() - ref.float()).norm() / ref.float().norm()).item(), out
 
 
+@pytest.mark.parametrize("wan_fp32", [False, True])
 @pytest.mark.parametrize("view_ids", [[0, 1, 2], [0, 2], [2, 1]])
-def test_crossview_tiny_matches_oracle(device, view_ids):
+def test_crossview_tiny_matches_oracle(device, view_ids, wan_fp32):
+    """wan_fp32=False: the registered cross-view net's bf16 conditioning (defaults/net.py:105); True: the fp32
+    strategy on the same layout."""
     cfg = tiny_dit(num_blocks=2, n_cameras_emb=3, state_t=2, adaln_view_embedding=True,
-                   cross_view_attn_map=((1, 2), (0,), (0, 1)))
+                   cross_view_attn_map=((1, 2), (0,), (0, 1)), use_wan_fp32_strategy=wan_fp32)
     rel, out = _case(device, cfg, view_ids, 2, 4, 8)
-    print(f"cross-view tiny net, views {view_ids}: rel-L2 {rel:.3e}")
+    print(f"cross-view tiny net, views {view_ids}, wan_fp32 {wan_fp32}: rel-L2 {rel:.3e}")
     assert torch.isfinite(out).all() and rel <= 1e-2, rel
 
 
@@ -67,7 +70,7 @@ def test_crossview_2b_width_seven_views(device):
     """The registered 2B cross-view net's widths and 7-view neighbour map (one block), 7 views x 8 latent frames of
     16 x 26 tokens (23 296 tokens, CFG-sized batch 1)."""
     cfg = dataclasses.replace(DIT_2B_MULTIVIEW_CROSSVIEW, num_blocks=1)
-    assert cfg.cross_view_attn_map == CROSS_VIEW_MAP_7
+    assert cfg.cross_view_attn_map == CROSS_VIEW_MAP_7 and not cfg.use_wan_fp32_strategy
     rel, out = _case(device, cfg, list(range(7)), 8, 16, 26)
     print(f"cross-view 2B-width block, 7 views: rel-L2 {rel:.3e}")
     assert torch.isfinite(out).all() and rel <= 1e-2, rel

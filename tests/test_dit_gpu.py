@@ -163,11 +163,14 @@ def test_action_dit_forward_matches_oracle(device, per_frame):
             condition_video_input_mask_B_C_T_H_W=mask.to(device))
 
 
-def test_multiview_dit_forward_matches_oracle(device):
+@pytest.mark.parametrize("wan_fp32", [False, True])
+def test_multiview_dit_forward_matches_oracle(device, wan_fp32):
     """Multi-view net (multiview_dit.py): 3 views x 2 latent frames stacked on T, view-embedding input
     channels (folded into a per-view bias on the device), per-view RoPE restart and per-view text
-    cross-attention (512 tokens each), joint self-attention; same tolerance as the plain forward."""
-    cfg = tiny_dit(num_blocks=2, n_cameras_emb=7, view_condition_dim=7, state_t=2)
+    cross-attention (512 tokens each), joint self-attention; same tolerance as the plain forward. wan_fp32=False is
+    the registered multi-view net's arithmetic (bf16 t-embedding / AdaLN / final layer, defaults/net.py:52); True the
+    fp32 strategy on the same layout."""
+    cfg = tiny_dit(num_blocks=2, n_cameras_emb=7, view_condition_dim=7, state_t=2, use_wan_fp32_strategy=wan_fp32)
     sd, sd_ref = _setup(cfg, seed=4)
     g = torch.Generator().manual_seed(14)
     V, T, H, W = 3, 6, 16, 16
@@ -182,7 +185,7 @@ def test_multiview_dit_forward_matches_oracle(device):
     out = net(x.to(device).to(torch.bfloat16), t.to(device), ctx.to(device),
               condition_video_input_mask_B_C_T_H_W=mask.to(device))
     err = rel_l2(out.cpu(), ref)
-    print(f"multiview dit forward (3 views) rel-L2: {err:.3e}")
+    print(f"multiview dit forward (3 views, wan_fp32 {wan_fp32}) rel-L2: {err:.3e}")
     assert err <= 1e-2, err
     # the views are distinguished: permuting the view embeddings changes the output
     sd2 = dict(sd_ref)

@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 
 
 def test_multiview_generate_shapes_and_conditioning(device):
-    cfg = tiny_dit(num_blocks=1, n_cameras_emb=7, view_condition_dim=7, state_t=2)
+    cfg = tiny_dit(num_blocks=1, n_cameras_emb=7, view_condition_dim=7, state_t=2, use_wan_fp32_strategy=False)
     pipe = Video2WorldInference("2B/auto/multiview", device=device, net_cfg=cfg,
                                 sampler_cfg=SamplerConfig(state_t=2, cfg_mode="text2world"))
     mv = MultiviewInference(pipe)
@@ -31,7 +31,7 @@ def test_multiview_generate_shapes_and_conditioning(device):
 def test_crossview_generate(device):
     """The cross-view net (MultiViewCrossDiT) through the same multi-view pipeline: 3 of the 7 rig views (ids 0, 1, 2:
     front_wide, cross_right, rear_right, so rear_right's neighbour rear_tele is absent and masked out)."""
-    cfg = tiny_dit(num_blocks=1, n_cameras_emb=7, state_t=2, adaln_view_embedding=True,
+    cfg = tiny_dit(num_blocks=1, n_cameras_emb=7, state_t=2, adaln_view_embedding=True, use_wan_fp32_strategy=False,
                    cross_view_attn_map=CROSS_VIEW_MAP_7)
     pipe = Video2WorldInference("2B/auto/multiview-crossview", device=device, net_cfg=cfg,
                                 sampler_cfg=SamplerConfig(state_t=2, cfg_mode="text2world"))
