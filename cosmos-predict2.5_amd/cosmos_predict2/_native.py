@@ -42,10 +42,26 @@ class UniPCParams(ctypes.Structure):
     ]
 
 
+class CP25Tensor(ctypes.Structure):
+    """Mirror of `cp25_tensor` (include/cp25.h): device pointer, CP25_DT_* dtype, rank, sizes, strides (elements)."""
+
+    _fields_ = [
+        ("data", ctypes.c_void_p),
+        ("dtype", ctypes.c_int32),
+        ("ndim", ctypes.c_int32),
+        ("shape", ctypes.c_int64 * 6),
+        ("strides", ctypes.c_int64 * 6),
+    ]
+
+
+DT_BF16, DT_F32, DT_F8E4M3, DT_U8 = 1, 2, 3, 4
+_DTYPES = {torch.bfloat16: DT_BF16, torch.float32: DT_F32, torch.float8_e4m3fn: DT_F8E4M3, torch.uint8: DT_U8}
+
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
 _I = ctypes.c_int
 _F = ctypes.c_float
+_T = ctypes.POINTER(CP25Tensor)
 
 # symbol -> argtypes (restype int, except the *_workspace_bytes queries)
 SIGNATURES = {
@@ -105,6 +121,9 @@ SIGNATURES = {
     "cp25_vae_attn": [_P, _I64, _I64, _P, _I64, _I64, _P, _I64, _I64, _P, _I64, _I64, _I, _I, _I, _I, _F, _P, _I64,
                       _P],
     "cp25_vae_attn_workspace_bytes": [_I, _I, _I, _I],
+    "cp25_attn_fwd_t": [_T, _T, _T, _T, _F, _P, ctypes.c_size_t, _P],
+    "cp25_gemm_epi_t": [_T, _T, _T, _I, _P],
+    "cp25_conv3d_t": [_T, _I, _T, _T, _T, _I, _I, _I, _I, _I, _I, _P],
 }
 
 
@@ -161,6 +180,58 @@ def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
 
 def _stream(device: torch.device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
+
+
+def tensor_desc(t: Optional[torch.Tensor]) -> Optional[CP25Tensor]:
+    """A cp25_tensor for a device tensor (data pointer, dtype, sizes, strides); None for None."""
+    if t is None:
+        return None
+    if t.dim() > 6:
+        raise ValueError(f"cp25_tensor holds at most 6 dimensions, got {t.dim()}")
+    if t.dtype not in _DTYPES:
+        raise ValueError(f"no cp25 dtype for {t.dtype}")
+    d = CP25Tensor()
+    d.data = _ptr(t)
+    d.dtype = _DTYPES[t.dtype]
+    d.ndim = t.dim()
+    for i in range(t.dim()):
+        d.shape[i] = t.shape[i]
+        d.strides[i] = t.stride(i)
+    return d
+
+
+def _ref(d: Optional[CP25Tensor]):
+    return None if d is None else ctypes.byref(d)
+
+
+def attn_fwd_t(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, o: torch.Tensor, softmax_scale: float,
+               workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """cp25_attn_fwd_t: the descriptor form of the attention (q / o [B, Lq, H, D], k / v [B, Lk, H, D] bf16); the
+    library checks dtypes and strides (ValueError on a mismatch)."""
+    lib = load_library()
+    ws = 0 if workspace is None else workspace.numel() * workspace.element_size()
+    _check("cp25_attn_fwd_t", lib.cp25_attn_fwd_t(*(_ref(tensor_desc(t)) for t in (q, k, v, o)), float(softmax_scale),
+                                                  _ptr(workspace), ws, _stream(q.device)))
+    return o
+
+
+def gemm_epi_t(a: torch.Tensor, w: torch.Tensor, c: torch.Tensor, epilogue: int = 0) -> torch.Tensor:
+    """cp25_gemm_epi_t: c [M, N] = epi(a [M, K] w [N, K]^T) over descriptors (EPI_NONE / EPI_GELU)."""
+    lib = load_library()
+    _check("cp25_gemm_epi_t", lib.cp25_gemm_epi_t(_ref(tensor_desc(a)), _ref(tensor_desc(w)), _ref(tensor_desc(c)),
+                                                  int(epilogue), _stream(a.device)))
+    return c
+
+
+def conv3d_t(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], out: torch.Tensor, *,
+             pad_front: int = 0, stride_t: int = 1, stride_hw: int = 1, pad: tuple = (0, 0, 0, 0)) -> torch.Tensor:
+    """cp25_conv3d_t: x [T, H, W, C] channels-last frames after pad_front zero frames, weight [Cout, KT, KH, KW, Cin],
+    bias [Cout] or None, out [Tout, Ho, Wo, Cout]; pad = (top, left, bottom, right)."""
+    lib = load_library()
+    _check("cp25_conv3d_t", lib.cp25_conv3d_t(_ref(tensor_desc(x)), int(pad_front), _ref(tensor_desc(weight)),
+                                              _ref(tensor_desc(bias)), _ref(tensor_desc(out)), stride_t, stride_hw,
+                                              pad[0], pad[1], pad[2], pad[3], _stream(x.device)))
+    return out
 
 
 def _i64x3(vals) -> ctypes.Array:

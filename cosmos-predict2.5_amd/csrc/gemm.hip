@@ -440,6 +440,7 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
   if (tile >= n_tiles) return;
   u32x4 nwv = {0u, 0u, 0u, 0u};  // CP25_EPI_HNORM: this lane's 8 norm weights (columns 8 (ch & 15) .. of its head)
   if constexpr (kEpi == CP25_EPI_HNORM || kEpi == CP25_EPI_QKV) nwv = *reinterpret_cast<const u32x4*>(re.nw + (tid & 15) * 8);
+#ifndef CP25_LAB_GELU_VALU
   if constexpr (kEpi == CP25_EPI_GELU) {  // the GELU table (visible after the prologue's barrier)
     unsigned short* tab = reinterpret_cast<unsigned short*>(smem + 2 * kBuf8);
     for (int i = tid; i < kGeluTab; i += kThreads) {
@@ -449,6 +450,7 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
+#endif
   int m0, n0;
   tile_mn(tile, m0, n0);
   set_tile(m0, n0);
@@ -649,6 +651,19 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
       issue_first_two();
     }
     __builtin_amdgcn_sched_barrier(0);  // the DMAs are queued ahead of the stores (the counts above rely on it)
+#ifdef CP25_LAB_GELU_VALU
+    if constexpr (kEpi == CP25_EPI_GELU) {  // lab (tools/lab/gelu): gelu_erf on every element, no table
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        u32x4 o;
+#pragma unroll
+        for (int w2 = 0; w2 < 4; ++w2)
+          o[w2] = (unsigned)f2bf(gelu_exact(bf2f((unsigned short)(cv[it][w2] & 0xffffu)))) |
+                  ((unsigned)f2bf(gelu_exact(bf2f((unsigned short)(cv[it][w2] >> 16)))) << 16);
+        cv[it] = o;
+      }
+    }
+#else
     if constexpr (kEpi == CP25_EPI_GELU) {
       // the GELU on the read-back bf16 products, by table (its own LDS region, untouched by the DMA just queued, so the
       // lookups run under that DMA's latency instead of in the C staging before it); one wave-wide test per 8-element
@@ -677,6 +692,7 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
         cv[it] = o;
       }
     }
+#endif
     if constexpr (kEpi == CP25_EPI_HNORM) {
       // lanes 16 h .. 16 h + 15 of a 32-lane row hold head h's 128 columns, lane li = ch & 15 the 8 columns 8 li ..:
       // cp25_head_rmsnorm_rope's item layout, so its butterfly over 16 lanes is this one (runs under the DMA above)

@@ -24,6 +24,46 @@
 extern "C" {
 #endif
 
+/* ---------------------------------------------------------------- tensor descriptors
+ * SURVEY.md §8(b)5's descriptor form, for the entry points a reference-side binding most often calls with
+ * framework tensors: cp25_attn_fwd_t, cp25_gemm_epi_t, cp25_conv3d_t. A descriptor carries the device pointer, the
+ * dtype, the rank and per-dimension sizes and strides (in elements). These entry points check every descriptor on
+ * the host and return CP25_ERR_DTYPE (-95) for a wrong dtype, CP25_ERR_INVAL (-22) for a rank / shape / stride /
+ * pointer mismatch, before any GPU work; then they run the pointer entry point of the same op. The other entry points
+ * keep plain pointers plus sizes (INTEGRATION.md §3 gives the reason). */
+#define CP25_MAX_DIMS 6
+#define CP25_DT_BF16 1
+#define CP25_DT_F32 2
+#define CP25_DT_F8E4M3 3
+#define CP25_DT_U8 4
+typedef struct cp25_tensor {
+  void* data;                      /* device pointer */
+  int32_t dtype;                   /* CP25_DT_* */
+  int32_t ndim;                    /* <= CP25_MAX_DIMS */
+  int64_t shape[CP25_MAX_DIMS];
+  int64_t strides[CP25_MAX_DIMS];  /* elements */
+} cp25_tensor;
+
+/* cp25_attn_fwd over descriptors: q / o [B, Lq, H, D], k / v [B, Lk, H, D], bf16, D = 128, unit head-dim stride. With
+ * a workspace of at least cp25_attn_workspace_bytes(B, H, Lq, cp25_attn_plan(B, H, Lq, Lk, D)) bytes the planned
+ * key-range split runs (cp25_attn_fwd_split), else the unsplit launch. Replaces: networks/attention.py:90-181. */
+int cp25_attn_fwd_t(const cp25_tensor* q, const cp25_tensor* k, const cp25_tensor* v, const cp25_tensor* o,
+                    float softmax_scale, void* workspace, size_t ws_bytes, hipStream_t stream);
+
+/* cp25_gemm_epi over descriptors: c [M, N] = epi(a [M, K] w [N, K]^T), bf16, unit inner strides; epilogue
+ * CP25_EPI_NONE or CP25_EPI_GELU (the other epilogues take more operands: cp25_gemm_res / _hnorm / _qkv).
+ * Replaces: block nn.Linear layers, minimal_v4_dit.py:227-254, 354-363, 401-432. */
+int cp25_gemm_epi_t(const cp25_tensor* a, const cp25_tensor* w, const cp25_tensor* c, int epilogue,
+                    hipStream_t stream);
+
+/* cp25_conv3d over descriptors: x [T, Hin, Win, Cin] channels-last frames (each contiguous, any frame stride) after
+ * pad_front zero frames (the causal padding), weight [Cout, KT, KH, KW, Cin], bias [Cout] or NULL, out contiguous
+ * [Tout, Ho, Wo, Cout] whose sizes must match the conv's, all bf16. Replaces: CausalConv3d.forward
+ * (tokenizers/wan2pt1.py:44-62). */
+int cp25_conv3d_t(const cp25_tensor* x, int pad_front, const cp25_tensor* weight, const cp25_tensor* bias,
+                  const cp25_tensor* out, int stride_t, int stride_hw, int pad_top, int pad_left, int pad_bottom,
+                  int pad_right, hipStream_t stream);
+
 /* ---------------------------------------------------------------- attention
  * softmax(Q K^T * softmax_scale) V, non-causal, no mask; bf16 in/out, fp32 accumulation.
  * q: [B, Lq, H, D] addressed by q_strides = {batch, token, head} (head dim contiguous), same for

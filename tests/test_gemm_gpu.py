@@ -42,6 +42,25 @@ def test_gemm_matches_fp32(device, M, Nn, K):
     assert torch.equal(N.gemm_epi(a[:m2].contiguous(), w), out[:m2])  # row results independent of M
 
 
+@pytest.mark.parametrize("K", [64, 2048])
+def test_gelu_epilogue_every_bf16_value(device, K):
+    """The GELU epilogue over every finite bf16 product (65 024 values; the epilogue's table range and the gelu_erf
+    fallback outside it) bit-identical to cp25_gelu: A's column 0 holds the values, W's column 0 is 1, so every
+    product is the value itself (one exact bf16 rounding) in each of the 256 output columns. K = 2048 runs the
+    persistent kernel (K / 64 even), K = 64 the one-tile-per-workgroup kernel."""
+    bits = torch.arange(0, 1 << 16, dtype=torch.int32).to(torch.int16).view(torch.bfloat16)
+    x = bits[torch.isfinite(bits.float())].to(device)
+    a = torch.zeros(x.numel(), K, dtype=torch.bfloat16, device=device)
+    a[:, 0] = x
+    w = torch.zeros(256, K, dtype=torch.bfloat16, device=device)
+    w[:, 0] = 1.0
+    assert torch.equal(N.gemm_epi(a, w)[:, 0], x)
+    g = N.gemm_epi(a, w, epilogue=N.EPI_GELU)
+    ref = x.clone()
+    N.gelu_(ref)
+    assert torch.equal(g, ref[:, None].expand(-1, 256))
+
+
 def test_gemm_strided_output_and_bad_shapes(device):
     a = torch.randn(300, 128, device=device).to(torch.bfloat16)
     w = torch.randn(512, 128, device=device).to(torch.bfloat16)

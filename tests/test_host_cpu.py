@@ -143,3 +143,58 @@ def test_unsupported_gemm_shape_raises():
     for shape in ((500, 384), (512, 100)):
         with pytest.raises(ValueError):
             _require_gemm(torch.empty(*shape))
+
+
+def _desc(dtype, shape, strides=None, data=0x100000):
+    """A cp25_tensor with a fake (never dereferenced) device address: the checks below fail before any GPU work."""
+    d = _native.CP25Tensor()
+    d.data, d.dtype, d.ndim = data, dtype, len(shape)
+    if strides is None:
+        strides, acc = [], 1
+        for n in reversed(shape):
+            strides.insert(0, acc)
+            acc *= n
+    for i, (n, st) in enumerate(zip(shape, strides)):
+        d.shape[i], d.strides[i] = n, st
+    return d
+
+
+def test_descriptor_abi_rejects_bad_dtypes_and_strides():
+    """the descriptor entry points return CP25_ERR_DTYPE (-95) for a wrong dtype
+    and CP25_ERR_INVAL (-22) for a shape / stride / pointer mismatch on the host, before anything touches a GPU (this
+    machine has none, so reaching a launch would fail differently)."""
+    lib = _native.load_library()
+    bf, f32 = _native.DT_BF16, _native.DT_F32
+    r = ctypes.byref
+    # attention: q fp32 where bf16 is required
+    q, k, v, o = (_desc(bf, (1, 300, 2, 128)) for _ in range(4))
+    assert lib.cp25_attn_fwd_t(r(_desc(f32, (1, 300, 2, 128))), r(k), r(v), r(o), 0.1, None, 0, None) == -95
+    assert lib.cp25_attn_fwd_t(r(q), r(k), r(_desc(_native.DT_F8E4M3, (1, 300, 2, 128))), r(o), 0.1, None, 0, None) == -95
+    assert lib.cp25_attn_fwd_t(r(q), r(k), r(v), r(_desc(bf, (1, 300, 2, 128), (76800, 256, 128, 2))), 0.1, None, 0,
+                               None) == -22  # head dim not contiguous
+    assert lib.cp25_attn_fwd_t(r(q), r(_desc(bf, (1, 299, 2, 128))), r(v), r(o), 0.1, None, 0, None) == -22  # k vs v
+    assert lib.cp25_attn_fwd_t(r(_desc(bf, (1, 300, 2, 64))), r(_desc(bf, (1, 300, 2, 64))), r(_desc(bf, (1, 300, 2, 64))),
+                               r(_desc(bf, (1, 300, 2, 64))), 0.1, None, 0, None) == -95  # head dim 64
+    assert lib.cp25_attn_fwd_t(None, r(k), r(v), r(o), 0.1, None, 0, None) == -22
+    # GEMM
+    a, w, c = _desc(bf, (512, 256)), _desc(bf, (256, 256)), _desc(bf, (512, 256))
+    assert lib.cp25_gemm_epi_t(r(_desc(f32, (512, 256))), r(w), r(c), 0, None) == -95
+    assert lib.cp25_gemm_epi_t(r(a), r(w), r(_desc(f32, (512, 256))), 0, None) == -95
+    assert lib.cp25_gemm_epi_t(r(a), r(_desc(bf, (256, 128))), r(c), 0, None) == -22  # K mismatch
+    assert lib.cp25_gemm_epi_t(r(a), r(w), r(_desc(bf, (512, 256), (1, 512))), 0, None) == -22  # column-major c
+    assert lib.cp25_gemm_epi_t(r(a), r(w), r(c), 2, None) == -22  # the residual epilogue needs its operands
+    assert lib.cp25_gemm_epi_t(r(_desc(bf, (512, 256), data=0)), r(w), r(c), 0, None) == -22  # null pointer
+    # conv
+    x, wt, b, out = _desc(bf, (4, 8, 8, 16)), _desc(bf, (32, 3, 3, 3, 16)), _desc(bf, (32,)), _desc(bf, (4, 8, 8, 32))
+    assert lib.cp25_conv3d_t(r(_desc(f32, (4, 8, 8, 16))), 2, r(wt), r(b), r(out), 1, 1, 1, 1, 1, 1, None) == -95
+    assert lib.cp25_conv3d_t(r(x), 2, r(wt), r(_desc(f32, (32,))), r(out), 1, 1, 1, 1, 1, 1, None) == -95
+    assert lib.cp25_conv3d_t(r(x), 2, r(wt), r(b), r(_desc(bf, (4, 8, 8, 31))), 1, 1, 1, 1, 1, 1, None) == -22
+    assert lib.cp25_conv3d_t(r(x), 0, r(wt), r(b), r(out), 1, 1, 1, 1, 1, 1, None) == -22  # too few frames for KT = 3
+    assert lib.cp25_conv3d_t(r(x), 2, r(wt), r(b), r(_desc(bf, (4, 7, 8, 32))), 1, 1, 1, 1, 1, 1, None) == -22  # Ho
+
+
+def test_tensor_desc_of_a_torch_tensor():
+    t = torch.zeros(3, 5, 7, dtype=torch.bfloat16)[:, 1:4]
+    with pytest.raises(RuntimeError):  # host tensors are refused like every other binding
+        _native.tensor_desc(t)
+    assert ctypes.sizeof(_native.CP25Tensor) == 8 + 4 + 4 + 6 * 8 * 2
