@@ -73,9 +73,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline threads (0: the host cores this process may use, capped by OMP_NUM_THREADS)")
-    ap.add_argument("--cpu-config1", action="store_true",
-                    help="also time BASELINE config 1 end to end on the CPU (~15 s; recorded once per round under "
-                         "profiles/, off by default so the driver's run stays short)")
+    ap.add_argument("--no-cpu-config1", action="store_true",
+                    help="skip the CPU leg's end-to-end BASELINE config 1 video (~30-60 s with the weight setup; on by "
+                         "default: the whole-video CPU baseline SURVEY.md §8(d) asks for)")
     ap.add_argument("--trained-evals", type=int, default=4,
                     help="N = 1: after the metric run, time this many evaluations with q/k norm weights uniform in "
                          "[0.5, 3] (the attention form a trained checkpoint gets) as the line's trained_norm_weights "
@@ -332,8 +332,10 @@ def main():
         threads, visible = host_threads(a.cpu_threads or None)
         cpu = dit_block_sample(L=state_t * (h // 16) * (w // 16), threads=threads, forwards=2 * evals, frames=frames)
         cpu["host_cores_visible"] = visible
-        if a.cpu_config1:
+        if not a.no_cpu_config1:
             cpu["config1_end_to_end"] = config1_end_to_end(threads=threads)
+        cpu["cores_note"] = (f"{threads} of {visible} host threads: the GPU box's CPU share for a one-GPU job is 16 "
+                             "(OMP_NUM_THREADS=16 there); its affinity mask lists every core of the shared host")
 
     if rank == 0:
         valid = (a.num_steps == 35 and a.frames == 121 and (h, w) == (704, 1280) and a.model == "2B/post-trained"
@@ -416,7 +418,7 @@ def main():
                 "flop_per_launch": attn_flop,
             },
             "cpu_baseline": cpu and {k: cpu[k] for k in ("value", "unit", "cores", "kind", "sample", "host_cores_visible",
-                                                         "sample_seconds", "config1_end_to_end") if k in cpu},
+                                                         "sample_seconds", "config1_end_to_end", "cores_note") if k in cpu},
         }
         if trained is not None:
             line["trained_norm_weights"] = trained
