@@ -491,7 +491,7 @@ class MinimalV1LVGDiT:
             self.w_view_proj = p["adaln_view_proj.weight"].float()
             self.b_view_proj = p["adaln_view_proj.bias"].float()
         self._bias_w = {}  # padded [w | bias | 0] copies for _bias_linear, per weight name
-        self._embed_f32 = None  # multi-view patch embedding: fp32 weight padded to K = 96, view-channel fold
+        self._embed_f32 = None  # multi-view patch embedding: fp32 weights padded to K % 32 == 0, view-channel fold
         self.refresh_norm_bounds()
         self._rope_cache.clear()
         if D % 512:
@@ -578,9 +578,10 @@ class MinimalV1LVGDiT:
         """bf16 nn.Linear with bias (weight / bias `key`.weight / .bias) of x [M, K] on the hand-written GEMM: the bias
         rides as one more K column (a' = [x | 1 | 0..], w' = [w | bias | 0..], K padded to a multiple of 64), so it
         enters the fp32 accumulator before the product's one bf16 rounding, as the library's bias epilogue adds it
-        (tests/test_gemm_f32_gpu.py: bit-identical to F.linear(bias) on its case). ValueError where the GEMM is not
-        built for the shape. The padded operand is a copy of x (for crossattn_proj: [B * 512, 100 416] bf16, ~0.2 GB,
-        once per prompt, freed on return)."""
+        (tests/test_gemm_f32_gpu.py: within 1 bf16 ulp of F.linear(bias), the two sum in different orders). ValueError
+        where the GEMM is not built for the shape. The padded weight replaces the state dict's weight (which becomes a
+        view of it), so the net holds one copy; the padded operand is a copy of x (for crossattn_proj: [B * 512,
+        100 416] bf16, ~0.2 GB, once per prompt, freed on return)."""
         p = self.sd
         w, bias = p[key + ".weight"], p[key + ".bias"]
         n_out, k_in = w.shape
@@ -594,6 +595,7 @@ class MinimalV1LVGDiT:
             wb[:, :k_in] = w
             wb[:, k_in] = bias
             self._bias_w[key] = wb
+            p[key + ".weight"] = wb[:, :k_in]  # one copy in HBM: the state dict's weight is now a view of wb
         a = torch.zeros((x.shape[0], kp), dtype=BF16, device=self.device)
         a[:, :k_in] = x
         a[:, k_in] = 1.0
@@ -795,23 +797,25 @@ class MinimalV1LVGDiT:
             view_indices = torch.arange(V, device=self.device)
         view_indices = view_indices.to(self.device).long().clamp(max=cfg.n_cameras_emb - 1)
         vdim = cfg.view_condition_dim
-        if self._embed_f32 is None:
-            # fp32 weights zero-padded to K = 96 (patch features) and 32 (the view channels folded over (p1, p2, t))
-            w96 = torch.zeros((D, 96), dtype=F32, device=self.device)
-            w96[:, :f] = w[:, :f]
-            wv = torch.zeros((D, 32), dtype=F32, device=self.device)
+        kf, kv = -(-f // 32) * 32, -(-vdim // 32) * 32  # cp25_gemm_f32 takes K % 32 == 0
+        if self._embed_f32 is None or self._embed_f32[0].shape[1] != kf:
+            # fp32 weights zero-padded to K = kf (patch features: 96 for the 72 of the 2B layout) and kv (the view
+            # channels folded over (p1, p2, t))
+            wk = torch.zeros((D, kf), dtype=F32, device=self.device)
+            wk[:, :f] = w[:, :f]
+            wv = torch.zeros((D, kv), dtype=F32, device=self.device)
             wv[:, :vdim] = w[:, f:].float().view(D, vdim, -1).sum(-1)
-            self._embed_f32 = (w96, wv)
-        w96, wv = self._embed_f32
-        emb = torch.zeros((V, 32), dtype=F32, device=self.device)
+            self._embed_f32 = (wk, wv)
+        wk, wv = self._embed_f32
+        emb = torch.zeros((V, kv), dtype=F32, device=self.device)
         emb[:, :vdim] = p["view_embeddings.weight"][view_indices]
         bias = N.gemm_f32(emb, wv)  # [V, D]
         view_of_tok = torch.arange(geo.tok0, geo.tok0 + n, device=self.device) // geo.L_view
-        rows = torch.zeros((n, Bx, 96), dtype=F32, device=self.device)
+        rows = torch.zeros((n, Bx, kf), dtype=F32, device=self.device)
         rows[:, :, :f] = patch_rows
-        # y[b] = rows[:, b] w96^T + bias[view of the token], batched over the Bx entries; fp32, rounded once
+        # y[b] = rows[:, b] wk^T + bias[view of the token], batched over the Bx entries; fp32, rounded once
         y = torch.empty((n, Bx, D), dtype=F32, device=self.device)
-        N.gemm_f32(rows.transpose(0, 1), w96.expand(Bx, D, 96), add=bias[view_of_tok].expand(Bx, n, D),
+        N.gemm_f32(rows.transpose(0, 1), wk.expand(Bx, D, kf), add=bias[view_of_tok].expand(Bx, n, D),
                    out=y.transpose(0, 1), split_k=False)
         return y.to(BF16)
 

@@ -18,12 +18,12 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 import isa_check  # noqa: E402
 
 CSRC = os.path.join(ROOT, "cosmos-predict2.5_amd", "csrc")
-SOURCES = ["attn_fwd.hip", "vae_ops.hip", "vae_attn.hip", "gemm.hip"]
+SOURCES = ["attn_fwd.hip", "vae_ops.hip", "vae_attn.hip", "gemm.hip", "gemm_f32.hip"]
 
 
 @pytest.fixture(scope="module", autouse=True)
 def _compile_all():
-    """Compile the four sources to ISA concurrently once (isa_check caches per source): the checks below then read the
+    """Compile the sources to ISA concurrently once (isa_check caches per source): the checks below then read the
     cache instead of waiting on one hipcc after another."""
     if not os.path.exists("/opt/rocm/bin/hipcc"):
         return
@@ -40,6 +40,16 @@ def test_no_lds_read_races(src):
     assert rep
     races = {n: r["races"][:2] for n, r in rep.items() if r["races"]}
     assert not races, races
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="hipcc not installed")
+def test_gemm_f32_no_inloop_scratch():
+    """cp25_gemm_f32's kernel double-buffers the W chunk in the LDS with one barrier per chunk: besides
+    the race check above, no scratch traffic inside its loops."""
+    rep = isa_check.check(os.path.join(CSRC, "gemm_f32.hip"))
+    assert rep
+    bad = {n: r["inloop_scratch"] for n, r in rep.items() if r["inloop_scratch"]}
+    assert not bad, bad
 
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="hipcc not installed")
