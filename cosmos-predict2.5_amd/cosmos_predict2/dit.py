@@ -183,6 +183,35 @@ class Geometry:
     tok0: int = 0  # first global token of this rank's shard
     n_tok: int = 0  # tokens on this rank
     n_views: int = 1  # multi-view: T = n_views x per-view frames, tokens ordered (view, t, h, w)
+    # frame-sharded rank (cross-view nets under context parallelism, frame_shard): the global frame of each local frame,
+    # local tokens ordered (view, local frame, h, w); None = the contiguous token range [tok0, tok0 + n_tok)
+    frames: Optional[Tuple[int, ...]] = None
+
+    @classmethod
+    def frame_shard(cls, T: int, Hp: int, Wp: int, n_views: int, rank: int, world: int) -> "Geometry":
+        """Rank `rank` of `world` holds frames [rank Tl, (rank + 1) Tl) of every view (Tl = T / n_views / world): the
+        reference's multi-view CP layout ("B C (c V T) H W", multiview_vid2vid_model_rectified_flow.py:400-403), in
+        which the cross-view attention of a frame needs no other rank (CrossViewAttention.set_context_parallel_group,
+        multiview_cross_dit.py:230-231) and each view's self-attention gathers the other ranks' frames."""
+        Tv = T // n_views
+        if T % n_views or Tv % world:
+            raise ValueError(f"{T} frames of {n_views} views do not shard by frame over {world} ranks")
+        Tl = Tv // world
+        frames = tuple(v * Tv + rank * Tl + t for v in range(n_views) for t in range(Tl))
+        return cls(T=T, Hp=Hp, Wp=Wp, tok0=0, n_tok=len(frames) * Hp * Wp, n_views=n_views, frames=frames)
+
+    def token_ids(self, device=None) -> torch.Tensor:
+        """Global token index of each local token."""
+        if self.frames is None:
+            return torch.arange(self.tok0, self.tok0 + self.n_tok, device=device)
+        f = torch.tensor(self.frames, device=device)
+        return (f[:, None] * self.hw + torch.arange(self.hw, device=device)[None, :]).reshape(-1)
+
+    def local(self) -> "Geometry":
+        """A frame-sharded rank's tokens as a geometry of their own (T = its frames, tok0 = 0); else self."""
+        if self.frames is None:
+            return self
+        return Geometry(T=len(self.frames), Hp=self.Hp, Wp=self.Wp, tok0=0, n_tok=self.n_tok, n_views=self.n_views)
 
     @property
     def T_view(self) -> int:
@@ -610,6 +639,9 @@ class MinimalV1LVGDiT:
             fr = fr.repeat(geo.n_views, 1).contiguous()
             self._rope_cache[key] = (torch.cos(fr).contiguous(), torch.sin(fr).contiguous())
         c, s = self._rope_cache[key]
+        if geo.frames is not None:  # a frame-sharded rank: its tokens' rows
+            idx = geo.token_ids(self.device)
+            return c[idx], s[idx]
         return c[geo.tok0: geo.tok0 + geo.n_tok], s[geo.tok0: geo.tok0 + geo.n_tok]
 
     # ---------------------------------------------------------------- fp32 conditioning
@@ -844,21 +876,38 @@ class MinimalV1LVGDiT:
         Bx = patch_rows.shape[1]
         x_in = self.embed_patches(patch_rows, geo, view_indices, rows_k128=rows_k128)
         mods, shift_f, scale_f = self.time_modulation(t_B_T, action)
+        cos, sin = self.rope_tables(geo)
+        sharded = geo.frames is not None
+        if sharded:
+            if not cfg.cross_view_attn_map:
+                raise ValueError("a frame-sharded geometry is the cross-view nets' CP layout")
+            # the rank's frames of the per-frame modulation, then everything below on the local geometry
+            fidx = torch.tensor(geo.frames, device=self.device)
+            mods, shift_f, scale_f = mods[:, :, :, fidx], shift_f[:, fidx], scale_f[:, fidx]
+            geo = geo.local()
         if cfg.adaln_view_embedding:
             mods = self._view_modulation(mods, geo, view_indices)
-        cos, sin = self.rope_tables(geo)
         cp = self.cp_group
         cp_size = 1 if cp is None else torch.distributed.get_world_size(cp)
+        cv = None
         if cfg.cross_view_attn_map:
-            if cp_size > 1 or geo.n_tok != geo.L:
-                raise NotImplementedError("cross-view nets run without context parallelism (one shard = all tokens)")
+            if geo.n_tok != geo.L or (cp_size > 1 and not sharded):
+                raise ValueError("cross-view nets shard by frame under context parallelism (Geometry.frame_shard)")
             cv = self._cross_view_neighbours(geo, view_indices)
-            gen = self._blocks(x_in, mods, shift_f, scale_f, ctx, geo, cos, sin, cp, cp_size, cv_nbrs=cv)
+        if B == 1 or (cp_size == 1 and not self.force_lanes) or (cv is not None and cp_size == 1):
+            gen = self._blocks(x_in, mods, shift_f, scale_f, ctx, geo, cos, sin, cp, cp_size, shared_batch,
+                               cv_nbrs=cv)
             while True:
                 try:
                     next(gen)
                 except StopIteration as e:
                     return e.value
+        if cv is not None:  # per-view self-attention gathers each view's frames; no shared block-0 prefix
+            lanes = [self._blocks(x_in[:, (0 if Bx == 1 else b):(0 if Bx == 1 else b) + 1], mods[:, :, b:b + 1],
+                                  shift_f[b:b + 1], scale_f[b:b + 1],
+                                  ContextCache(B=1, k=[t[b:b + 1] for t in ctx.k], v=[t[b:b + 1] for t in ctx.v]), geo,
+                                  cos, sin, cp, cp_size, cv_nbrs=cv) for b in range(B)]
+            return torch.cat(run_lanes(lanes), dim=1)
         if B == 1 or (cp_size == 1 and not self.force_lanes):
             gen = self._blocks(x_in, mods, shift_f, scale_f, ctx, geo, cos, sin, cp, cp_size, shared_batch)
             while True:
@@ -1046,8 +1095,9 @@ class MinimalV1LVGDiT:
                     lk = kk.shape[1] if cv_nbrs is None else geo.L_view
                 else:
                     yield from self._cp_self_attention(i, h, o, cos, sin, n, B, cp, cp_size,
-                                                       ev[0] if ev is not None else None)
-                    lk = cp_size * n
+                                                       ev[0] if ev is not None else None,
+                                                       views=geo if cv_nbrs is not None else None)
+                    lk = cp_size * (n if cv_nbrs is None else geo.L_view)
                 if ev is not None:
                     ev[1].record()
                     self.attn_events.append((ev[0], ev[1], 4.0 * Bs * H * n * lk * hd))
@@ -1153,11 +1203,13 @@ class MinimalV1LVGDiT:
         return torch.empty(shape, dtype=BF16, device=self.device)
 
     def _cp_self_attention(self, i: int, h: torch.Tensor, o: torch.Tensor, cos, sin, n: int, B: int, cp,
-                           cp_size: int, e0=None):
+                           cp_size: int, e0=None, views: Optional[Geometry] = None):
         """Self-attention of a context-parallel token shard (replaces the reference's Ulysses
         all-to-all, a2a_cp.py:160-219, which needs T % cp == 0): the shard's normed + roped K|V rows
         are all-gathered from every rank over RCCL, asynchronously (the other lane computes
-        meanwhile); the attention waits for the gather only. Same QKV GEMM and norm as CP = 1."""
+        meanwhile); the attention waits for the gather only. Same QKV GEMM and norm as CP = 1.
+        views (a frame-sharded cross-view rank's local geometry): per-view self-attention, view v's keys are every
+        rank's rows of view v in rank order, i.e. in frame order (copied into one sequence per view)."""
         cfg = self.cfg
         p = self.sd
         pre = f"blocks.{i}."
@@ -1185,6 +1237,22 @@ class MinimalV1LVGDiT:
         if w_ev is not None:
             w_ev[1].record()
             self.comm_events.append(w_ev)
+        if views is not None:
+            if self.attention_precision != "bf16":
+                raise NotImplementedError("the fp8 attention forms are not built for per-view self-attention")
+            if e0 is not None:
+                e0.record()
+            V, Lv = views.n_views, views.L_view
+            q = qkv.view(n, B, 3 * D)[:, :, :D].view(n, B, H, hd).transpose(0, 1)
+            ov = o.view(n, B, H, hd).transpose(0, 1)
+            kv5 = kv_all.view(cp_size, V, Lv * B, 2 * D)
+            qn = attn_kw.get("q_norm")
+            for vi in range(V):
+                kc, vc = kv_chunk_views(kv5[:, vi].reshape(cp_size * Lv * B, 2 * D), cp_size * Lv, B, H, hd)
+                sl = slice(vi * Lv, (vi + 1) * Lv)
+                kw = attn_kw if qn is None else dict(attn_kw, q_norm=dict(qn, cos=qn["cos"][sl], sin=qn["sin"][sl]))
+                N.attn_fwd(q[:, sl], kc, vc, out=ov[:, sl], **kw)
+            return
         kc, vc = kv_chunk_views(kv_all, cp_size * n, B, H, hd)
         attn_kw = self._fp8_qk(qkv[:, :D], kv_all[:, :D], B, H, hd, attn_kw, vc)
         if e0 is not None:

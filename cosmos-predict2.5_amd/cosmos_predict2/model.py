@@ -227,9 +227,14 @@ class SamplingRun:
         rank, world = (0, 1) if cp is None else (torch.distributed.get_rank(cp), torch.distributed.get_world_size(cp))
         if L % world:
             raise ValueError(f"token count {L} not divisible by the context-parallel size {world}")
-        geo.n_tok = L // world
-        geo.tok0 = rank * geo.n_tok
-        sl = slice(geo.tok0, geo.tok0 + geo.n_tok)
+        if world > 1 and model.net.cfg.cross_view_attn_map:
+            # cross-view nets shard by frame: every view's frames [rank Tl, (rank + 1) Tl) (Geometry.frame_shard)
+            geo = Geometry.frame_shard(T, H // 2, W // 2, geo.n_views, rank, world)
+            sl = geo.token_ids(dev)
+        else:
+            geo.n_tok = L // world
+            geo.tok0 = rank * geo.n_tok
+            sl = slice(geo.tok0, geo.tok0 + geo.n_tok)
         self.geo, self.cp, self.world = geo, cp, world
 
         noise_full = arch_invariant_rand((1, C, T, H, W), torch.float32, dev, seed)
@@ -242,6 +247,9 @@ class SamplingRun:
             for vi in range(geo.n_views):
                 frame_mask[vi * geo.T_view: vi * geo.T_view + num_conditional_frames] = 1.0
         self.frame_mask = frame_mask
+        # the per-token kernels (patchify, cfg_velocity) index the mask by (tok0 + token) // hw: a frame-sharded rank
+        # passes its own frames' entries with tok0 = 0
+        self.kmask = frame_mask if geo.frames is None else frame_mask[list(geo.frames)].contiguous()
         self.gtp = None
         if gt is not None and num_conditional_frames > 0:
             self.gtp = to_patch_layout(gt[0].to(dev, torch.float32))[sl].contiguous()
@@ -282,7 +290,7 @@ class SamplingRun:
             raise RuntimeError("the trajectory is complete (restart() to run it again)")
         m, geo = self.model, self.geo
         t = self.timesteps[self.i]
-        rows = N.patchify(self.x, self.gtp, self.frame_mask, None, tok0=geo.tok0, hw=geo.hw, ld=128)
+        rows = N.patchify(self.x, self.gtp, self.kmask, None, tok0=geo.tok0, hw=geo.hw, ld=128)
         tf = m._frame_timesteps(t, self.frame_mask)  # [T]
         t_B_T = m.net.scale_timesteps(tf[None, :]).expand(2, geo.T).contiguous()
         if self.net_fn is None:
@@ -292,7 +300,7 @@ class SamplingRun:
                                            view_indices=self.view_indices, shared_batch=shared, rows_k128=True)
         else:
             net_out = self.net_fn(rows.view(geo.n_tok, 1, -1), t_B_T, geo)
-        v = N.cfg_velocity(net_out, self.noise, self.gtp, self.frame_mask, self.guidance, self.mode,
+        v = N.cfg_velocity(net_out, self.noise, self.gtp, self.kmask, self.guidance, self.mode,
                            tok0=geo.tok0, hw=geo.hw)
         del net_out
         self.sched.step_(v, t)
@@ -305,5 +313,13 @@ class SamplingRun:
         x = self.x
         if self.world > 1:
             x = cpu.gather_tokens(x, self.cp)
+            if self.geo.frames is not None:  # frame-sharded ranks: back to the global (view, frame, h, w) order
+                C_, T_, H_, W_ = self.state_shape
+                g = self.geo
+                ids = torch.cat([Geometry.frame_shard(T_, g.Hp, g.Wp, g.n_views, r, self.world).token_ids(x.device)
+                                 for r in range(self.world)])
+                xg = torch.empty_like(x)
+                xg[ids] = x
+                x = xg
         _, T, H, W = self.state_shape
         return from_patch_layout(x, T, H, W).unsqueeze(0)

@@ -140,3 +140,71 @@ def test_cp2_matches_cp1(device, monkeypatch, world, split_env, tol, precision):
     err = ((res[0] - ref).norm() / ref.norm()).item()
     print(f"CP={world} vs CP=1 sampler rel-L2 (CP25_ATTN_SPLIT={split_env or 'plan'}, {precision}): {err:.3e}")
     assert err <= tol, err
+
+
+def _crossview_case():
+    from cosmos_predict2.dit import init_state_dict
+    from cosmos_predict2.net_config import SamplerConfig, tiny_dit
+
+    V, Tv = 3, 2
+    cfg = tiny_dit(num_blocks=2, n_cameras_emb=3, state_t=Tv, adaln_view_embedding=True,
+                   cross_view_attn_map=((1, 2), (0,), (0, 1)), use_wan_fp32_strategy=False)
+    sd = {"net." + k: v for k, v in init_state_dict(cfg, seed=4, zero_adaln_out=False).items()}
+    g = torch.Generator().manual_seed(31)
+    T, H, W = V * Tv, 16, 32
+    gt = torch.randn(1, 16, T, H, W, generator=g)
+    cc = torch.randn(1, 512 * V, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
+    cu = torch.randn(1, 512 * V, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
+    scfg = SamplerConfig(use_kerras_sigma_at_inference=True, conditional_frame_timestep=0.1, state_t=Tv,
+                         cfg_mode="text2world")
+    return cfg, scfg, sd, gt, cc, cu, (16, T, H, W), torch.tensor([2, 0, 1])
+
+
+def _crossview_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    N.set_attn_split(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from cosmos_predict2.model import Video2WorldModelRectifiedFlow
+
+        dev = torch.device("cuda:0")
+        cfg, scfg, sd, gt, cc, cu, shape, vi = _crossview_case()
+        m = Video2WorldModelRectifiedFlow(cfg, scfg, device=dev)
+        m.load_state_dict(sd)
+        m.set_context_parallel_group(dist.group.WORLD)
+        out = m.sample_latents(gt.to(dev), cc.to(dev), cu.to(dev), state_shape=shape, num_conditional_frames=1,
+                               guidance=0.0, seed=0, num_steps=2, view_indices=vi.to(dev)).cpu()
+        q.put((rank, out.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_crossview_cp2_matches_cp1(device, monkeypatch):
+    """The cross-view net (MultiViewCrossDiT) at CP = 2: each rank holds frame 0 or 1 of every view
+    (Geometry.frame_shard: the cross-view attention of a frame is local, each view's self-attention gathers the other
+    rank's frame of the view), two ranks over gloo sharing cuda:0, the sampler's gathered latent against CP = 1 bit for
+    bit (CP25_ATTN_SPLIT=1: the same key order and no split in every attention row)."""
+    from cosmos_predict2.model import Video2WorldModelRectifiedFlow
+
+    monkeypatch.setattr(N, "_ATTN_SPLIT", 1)
+    cfg, scfg, sd, gt, cc, cu, shape, vi = _crossview_case()
+    m = Video2WorldModelRectifiedFlow(cfg, scfg, device=device)
+    m.load_state_dict(sd)
+    ref = m.sample_latents(gt.to(device), cc.to(device), cu.to(device), state_shape=shape, num_conditional_frames=1,
+                           guidance=0.0, seed=0, num_steps=2, view_indices=vi.to(device)).cpu()
+    del m
+    torch.cuda.empty_cache()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_crossview_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {r: torch.from_numpy(a) for r, a in (q.get(timeout=100) for _ in ps)}
+    for p in ps:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in ps)
+    assert torch.equal(res[0], res[1])
+    err = ((res[0] - ref).norm() / ref.norm()).item()
+    print(f"cross-view CP=2 vs CP=1 sampler rel-L2 (CP25_ATTN_SPLIT=1): {err:.3e}")
+    assert torch.isfinite(ref).all() and err == 0.0, err
