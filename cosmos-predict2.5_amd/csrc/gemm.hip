@@ -303,6 +303,50 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
     m0 = (first_m + (tile % (gm * nt)) % gsize) * kBM;
     n0 = ((tile % (gm * nt)) / gsize) * kBN;
   };
+  // Tail plan (round 6): the F full rounds of the grid's P workgroups run whole tiles; the R tiles of the last, partial
+  // round run as s row slices of 256 / s rows each when they fit in one round of slices: s = 4 if 4 R <= P, 2 if
+  // 2 R <= P, else whole tiles. A slice is not s times cheaper: it still streams the whole W tile, runs every phase's
+  // barriers and the whole epilogue; measured (tools/lab/gemm_tail/ab_tail.py, profiles/r6/gemm_tail/) a half slice
+  // costs ~0.72 and a quarter ~0.55 of a tile (more with the GELU epilogue), so two rounds of slices never beat one
+  // round of tiles. E.g. a CP = 8 rank's QKV (1296 tiles on 256 CUs: 16 left) runs 64 quarter slices, the whole
+  // CFG batch's 2048-wide projections (856 tiles: 88 left) 176 halves. A slice is its parent tile with the rows outside it masked: the same LDS
+  // image, DMA and phase schedule, MFMAs only for the slice's rows (a half tile: the first A half; a quarter: its first
+  // wave row), so every output element is the same MFMA chain in the same K order as in a whole tile: rows stay
+  // independent of M and of the plan (tests/test_gemm_gpu.py, test_configs_net_gpu.py CP = 8 rows).
+  // The plan is recomputed at each tile seam from the launch's own values instead of being kept: the K loop sits at the
+  // SGPR limit, and five more live scalars pushed the buffer descriptors into VGPRs (a readfirstlane waterfall per DMA
+  // issue, +12 %). P is laundered so the compiler cannot hoist the plan out of the tile loop.
+  auto plan = [&](int& FP, int& sd, int& nv) __attribute__((always_inline)) {
+    int Pl = gridDim.x;
+    asm volatile("" : "+s"(Pl));
+    const int F = n_tiles / Pl, R = n_tiles - F * Pl;
+    sd = 4 * R <= Pl ? 4 : (2 * R <= Pl ? 2 : 1);
+    FP = F * Pl;
+    nv = FP + R * sd;
+  };
+  // virtual tile v -> (m0, n0, rows of the slice); wave-uniform by construction and said so (readfirstlane), or the
+  // buffer descriptors built from them count as divergent
+  auto tile_at = [&](int v, int& m0, int& n0, int& rows) __attribute__((always_inline)) {
+    int FP, sd, nv;
+    plan(FP, sd, nv);
+    if (v < FP) {
+      tile_mn(v, m0, n0);
+      rows = kBM;
+    } else {
+      const int j = v - FP;
+      tile_mn(FP + j / sd, m0, n0);
+      rows = kBM / sd;
+      m0 += (j % sd) * rows;
+    }
+    m0 = __builtin_amdgcn_readfirstlane(m0);
+    n0 = __builtin_amdgcn_readfirstlane(n0);
+    rows = __builtin_amdgcn_readfirstlane(rows);
+  };
+  auto n_virtual = [&]() __attribute__((always_inline)) {
+    int FP, sd, nv;
+    plan(FP, sd, nv);
+    return nv;
+  };
 
   // ---- DMA (buffer_load ... lds): wave w fills pieces 2w, 2w+1 (8 rows each) of every half-tile; lane l -> row
   // l/8 of the piece, LDS chunk l%8, global chunk (l%8) ^ swz(row), swz(row) = (row >> 1) & 7. A's descriptor ends
@@ -318,9 +362,15 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
     for (int h = 0; h < 2; ++h) a_vo[h][j] = ((2 * wave + j) * 8 + h * 128 + prow) * (int)lda * kES + c * 16;
   }
   __amdgpu_buffer_rsrc_t a_rsrc, w_rsrc;
-  auto set_tile = [&](int m0, int n0) __attribute__((always_inline)) {
-    a_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)A + (int64_t)m0 * lda * kES), (short)0,
-                                               (int)((int64_t)min(M - m0, kBM) * lda * kES), 0x00020000);
+  // m_lim: the tile's row end, M or the end of its slice (rows past it read as zeros and are not stored). A slice of the
+  // ragged last row tile may lie wholly past M (m_lim < m0): its descriptors then cover nothing (every clamp below
+  // keeps its loads in bounds), its MFMAs run on zeros and it stores nothing.
+  auto set_tile = [&](int m0, int n0, int m_lim) __attribute__((always_inline)) {
+    // (the bound through readfirstlane: computed from the slice's row end it otherwise counts as divergent, and a
+    // divergent descriptor turns every DMA issue of the K loop into a waterfall loop)
+    const int a_bytes = __builtin_amdgcn_readfirstlane((int)((int64_t)max(0, min(m_lim - m0, kBM)) * lda * kES));
+    a_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)A + (int64_t)m0 * lda * kES), (short)0, a_bytes,
+                                               0x00020000);
     w_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)W + (int64_t)n0 * ldw * kES), (short)0,
                                                (int)((int64_t)kBN * ldw * kES), 0x00020000);
   };
@@ -340,11 +390,12 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
   // fp8: the tile's scales ride the DMA queue ahead of K-tile 0 (one dword per lane: waves 0-3 the 256 row scales of
   // A -- rows past M read 0 from the descriptor bound --, waves 4-7 the 256 column scales of W), so the epilogue
   // reads them from the LDS instead of paying a global-load round trip per tile. Retired with K-tile 0.
-  auto issue_scales = [&](int m0, int n0) __attribute__((always_inline)) {
+  auto issue_scales = [&](int m0, int n0, int m_lim) __attribute__((always_inline)) {
     if constexpr (kES == 1) {
       const bool is_a = wave < 4;
       const __amdgpu_buffer_rsrc_t s_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(is_a ? a_scale + m0 : w_scale + n0), (short)0, is_a ? min(M - m0, kBM) * 4 : kBN * 4, 0x00020000);
+          (void*)(is_a ? a_scale + m0 : w_scale + n0), (short)0,
+          __builtin_amdgcn_readfirstlane(is_a ? max(0, min(m_lim - m0, kBM)) * 4 : kBN * 4), 0x00020000);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(s_rsrc, (lds_void_ptr)(smem + 2 * kBuf8 + wave * 256), 4,
                                                ((wave & 3) * 64 + lane) * 4, 0, 0, 0);  // bound-checked offset
     }
@@ -365,9 +416,11 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
   f32x4_t acc[2][2][4][2];
   bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
   bool stores_pending = false;  // this wave's previous-tile C stores are in flight, queued after K-tiles 0 and 1
+  int t_rows = kBM;             // rows of the current tile (kBM, or a tail slice's; tile_at): read by the slice loop only
 
-  auto phase = [&](auto qc, auto bc, int kt) __attribute__((always_inline)) {
+  auto phase = [&](auto qc, auto bc, int kt, auto slc) __attribute__((always_inline)) {
     constexpr int Q = decltype(qc)::value, BUF = decltype(bc)::value;
+    constexpr bool kSlice = decltype(slc)::value;  // a tail row slice (tile_at): the K loop's second instance
     const char* sbuf = smem + BUF * kBuf8;
     if constexpr (Q == 0 || Q == 1) {
       const char* sb = sbuf + 2 * kHalf + Q * kHalf + b_row;
@@ -410,7 +463,10 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
     __builtin_amdgcn_s_setprio(1);
     constexpr int mq = Q >> 1, nq = (Q == 1 || Q == 2);
     auto& fb = nq ? fb1 : fb0;
-    if constexpr (kES == 1) {
+    // a row slice of the tail (tile_at): only the waves / A half holding its rows issue MFMAs (wave-uniform; whole
+    // tiles run the K loop instance without this test)
+    if (kSlice && !(mq == 0 && (t_rows == kBM / 2 || wr == 0))) {
+    } else if constexpr (kES == 1) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -437,7 +493,7 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
   };
 
   int tile = my_slot;
-  if (tile >= n_tiles) return;
+  if (tile >= n_virtual()) return;
   u32x4 nwv = {0u, 0u, 0u, 0u};  // CP25_EPI_HNORM: this lane's 8 norm weights (columns 8 (ch & 15) .. of its head)
   if constexpr (kEpi == CP25_EPI_HNORM || kEpi == CP25_EPI_QKV) nwv = *reinterpret_cast<const u32x4*>(re.nw + (tid & 15) * 8);
 #ifndef CP25_LAB_GELU_VALU
@@ -452,9 +508,9 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
   }
 #endif
   int m0, n0;
-  tile_mn(tile, m0, n0);
-  set_tile(m0, n0);
-  issue_scales(m0, n0);
+  tile_at(tile, m0, n0, t_rows);
+  set_tile(m0, n0, min(M, m0 + t_rows));
+  issue_scales(m0, n0, min(M, m0 + t_rows));
   issue_first_two();
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // K-tile 0 (and the fp8 scales)
   __builtin_amdgcn_s_barrier();
@@ -474,15 +530,27 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
           for (int j = 0; j < 2; ++j) acc[mq][nq][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger the second wave group by one barrier
     __builtin_amdgcn_sched_barrier(0);
-    for (int kt = 0; kt < nk; kt += 2) {
-      phase(I0{}, I0{}, kt);
-      phase(I1{}, I0{}, kt);
-      phase(I2{}, I0{}, kt);
-      phase(I3{}, I0{}, kt);
-      phase(I0{}, I1{}, kt + 1);
-      phase(I1{}, I1{}, kt + 1);
-      phase(I2{}, I1{}, kt + 1);
-      phase(I3{}, I1{}, kt + 1);
+    auto kloop = [&](auto slc) __attribute__((always_inline)) {
+      for (int kt = 0; kt < nk; kt += 2) {
+        phase(I0{}, I0{}, kt, slc);
+        phase(I1{}, I0{}, kt, slc);
+        phase(I2{}, I0{}, kt, slc);
+        phase(I3{}, I0{}, kt, slc);
+        phase(I0{}, I1{}, kt + 1, slc);
+        phase(I1{}, I1{}, kt + 1, slc);
+        phase(I2{}, I1{}, kt + 1, slc);
+        phase(I3{}, I1{}, kt + 1, slc);
+      }
+    };
+    if (t_rows == kBM)
+      kloop(std::false_type{});
+    else
+      kloop(std::true_type{});
+    int m_lim;
+    {
+      int m0_, n0_, rows_;
+      tile_at(tile, m0_, n0_, rows_);
+      m_lim = min(M, m0 + rows_);
     }
     if (wr == 0) __builtin_amdgcn_s_barrier();
     // every wave's reads of this tile are done and no DMA is in flight: the LDS becomes the C tile. Raw barriers
@@ -491,7 +559,7 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
     __builtin_amdgcn_s_barrier();
 
     const int next = tile + gridDim.x;
-    const bool has_next = next < n_tiles;
+    const bool has_next = next < n_virtual();
     // ---- C tile -> LDS [256][256] bf16 (row stride 512 B; 16-B chunk ch of row r at ch ^ sw(r), sw(r) =
     // 2 ((r >> 2) & 3) = 2 fg for this wave's rows, so the four row groups of a fragment write hit distinct banks).
     // Element (row, col): row = mq 128 + wr 64 + 16 i + 4 fg + r, col = nq 128 + wc 32 + 16 j + fr; the lane part
@@ -504,9 +572,9 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
     const int ch = tid & 31, r0 = tid >> 5;
     u32x4 xres[16], gres[16];
     if constexpr (kEpi == CP25_EPI_RES) {
-      const int row_a = min(m0 + r0, M - 1), tok_a = row_a / re.B, b = row_a % re.B, dtok = 16 / re.B;
+      const int row_a = min(m0 + r0, m_lim - 1), tok_a = row_a / re.B, b = row_a % re.B, dtok = 16 / re.B;
       const unsigned short* xp = re.x + (int64_t)tok_a * re.x_st + b * re.x_sb + n0 + ch * 8;
-      const int n_valid = (M - 1 - row_a) / 16;  // rows row_a + 16 it, it <= n_valid, exist
+      const int n_valid = (m_lim - 1 - row_a) / 16;  // rows row_a + 16 it, it <= n_valid, exist
       // the row offset is selected arithmetically (x 0 or 1): a selected POINTER made the compiler load the fallback
       // row first and branch around a second load behind a vmcnt(0) -- sixteen serialised HBM round trips per tile
 #pragma unroll
@@ -544,10 +612,10 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
       // row r0 + 16 it: token tok_a + it * (16 / B), batch entry b (16 % B == 0), frame by a running remainder that
       // wraps at most once per step (16 / B <= hw, host-checked): straight-line code. Rows past M (a ragged last
       // row-tile) read the thread's first valid row instead (their results are not stored).
-      const int row_a = min(m0 + r0, M - 1), tok_a = row_a / re.B, b = row_a % re.B, dtok = 16 / re.B;
+      const int row_a = min(m0 + r0, m_lim - 1), tok_a = row_a / re.B, b = row_a % re.B, dtok = 16 / re.B;
       int64_t fr = (re.tok0 + tok_a) / re.hw, rem = (re.tok0 + tok_a) % re.hw;
       const unsigned short* gp = re.gate + b * re.g_sb + n0 + ch * 8;
-      const int n_valid = (M - 1 - row_a) / 16;  // rows row_a + 16 it, it <= n_valid, exist
+      const int n_valid = (m_lim - 1 - row_a) / 16;  // rows row_a + 16 it, it <= n_valid, exist
 #pragma unroll
       for (int it = 0; it < 16; ++it) {
         const bool ok = it <= n_valid;
@@ -578,7 +646,7 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
         const int tok_lo = m0 / re.B;
         constexpr int kTabBytes = 65536;  // per table: up to 256 tokens x 64 fp32
         if (rope) {
-          const int ntok = min(M - 1, m0 + kBM - 1) / re.B - tok_lo + 1;
+          const int ntok = max(0, min(m_lim - 1, m0 + kBM - 1) / re.B - tok_lo + 1);
           const int nbytes = ntok * 256;
           const __amdgpu_buffer_rsrc_t c_rsrc = __builtin_amdgcn_make_buffer_rsrc(
               (void*)(re.rcos + (int64_t)tok_lo * 64), (short)0, nbytes, 0x00020000);
@@ -609,7 +677,7 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
           for (int e = 0; e < 8; ++e)
             v[e] = hn_norm(v[e], rstd, bf2f((unsigned short)(nwv[e >> 1] >> (16 * (e & 1)))));
           if (rope) {
-            const int tl = min(m0 + r0 + 16 * it, M - 1) / re.B - tok_lo;
+            const int tl = max(0, min(m0 + r0 + 16 * it, m_lim - 1) / re.B - tok_lo);
             const f32x4 c0 = *reinterpret_cast<const f32x4*>(tcos + tl * 64 + dlo);
             const f32x4 c1 = *reinterpret_cast<const f32x4*>(tcos + tl * 64 + dlo + 4);
             const f32x4 s0 = *reinterpret_cast<const f32x4*>(tsin + tl * 64 + dlo);
@@ -637,17 +705,17 @@ gemm_nt_8ph(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the x / gate chunks (nothing else is in flight)
 #pragma unroll
       for (int it = 0; it < 16; ++it)
-        if (m0 + r0 + 16 * it < M) cv[it] = res8(cv[it], xres[it], gres[it]);
+        if (m0 + r0 + 16 * it < m_lim) cv[it] = res8(cv[it], xres[it], gres[it]);
     }
 
     unsigned short* crow = C + (int64_t)(m0 + r0) * ldc + n0 + ch * 8;
-    const bool full = m0 + kBM <= M;
-    const int rows_left = M - (m0 + r0);  // rows of C from this lane's first row (ragged last row-tile)
+    const bool full = m0 + kBM <= m_lim;
+    const int rows_left = m_lim - (m0 + r0);  // rows of C from this lane's first row (ragged last row-tile / slice)
     if (has_next) {
       tile = next;
-      tile_mn(tile, m0, n0);
-      set_tile(m0, n0);
-      issue_scales(m0, n0);
+      tile_at(tile, m0, n0, t_rows);
+      set_tile(m0, n0, min(M, m0 + t_rows));
+      issue_scales(m0, n0, min(M, m0 + t_rows));
       issue_first_two();
     }
     __builtin_amdgcn_sched_barrier(0);  // the DMAs are queued ahead of the stores (the counts above rely on it)
@@ -775,7 +843,8 @@ static int gemm_launch(const void* a, int64_t lda, const void* w, int64_t ldw, v
   if (!n_cu[dev] && hipDeviceGetAttribute(&n_cu[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return CP25_ERR_LAUNCH;
   const int cus = n_cu[dev] >= 8 ? n_cu[dev] & ~7 : n_cu[dev];
-  const dim3 pgrid((unsigned)std::min<int64_t>(nwg, cus));
+  // (up to 4 x the tiles: with fewer tiles than CUs the kernel's tail plan runs them as row slices)
+  const dim3 pgrid((unsigned)std::min<int64_t>(4 * nwg, cus));
   if ((K / kBK) % 2 != 0) {
     switch (epilogue) {
       case CP25_EPI_GELU:
@@ -836,7 +905,7 @@ static int gemm_fp8_launch(const void* a, int64_t lda, const float* a_scale, con
   if (!n_cu[dev] && hipDeviceGetAttribute(&n_cu[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return CP25_ERR_LAUNCH;
   const int cus = n_cu[dev] >= 8 ? n_cu[dev] & ~7 : n_cu[dev];
-  const dim3 pgrid((unsigned)std::min<int64_t>(nwg, cus)), block(kThreads);
+  const dim3 pgrid((unsigned)std::min<int64_t>(4 * nwg, cus)), block(kThreads);  // (tail row slices: gemm_launch)
   auto* A = (const unsigned short*)a;
   auto* Wp = (const unsigned short*)w;
   auto* Cp = (unsigned short*)c;

@@ -47,7 +47,11 @@ def main():
     ap.add_argument("--batch1", action="store_true", help="debug: one batch entry (no lanes)")
     ap.add_argument("--no-phase", action="store_true", help="debug: never record lane 0's phase event")
     ap.add_argument("--force-lanes", action="store_true", help="run the two lanes at CP = 1 too")
+    ap.add_argument("--lib", default="", help="a lab build of libcp25.so to load instead of the in-tree one (A/B)")
     a = ap.parse_args()
+    if a.lib:
+        from cosmos_predict2 import _native
+        _native._LIB_PATH = a.lib
     faulthandler.dump_traceback_later(90, repeat=True)  # a stuck host shows where
     dev = torch.device("cuda:0")
     cfg = MODELS[a.model][0]
