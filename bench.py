@@ -41,7 +41,7 @@ HIPBLASLT_BEST_BF16_TFLOPS = 1499.4  # measured: hipBLASLt bf16 16384^3, random 
 # measured: register-only v_mfma_f32_16x16x32_bf16 loop on random data, no memory traffic at all (the shape the
 # self-attention kernel runs; tools/lab/mfma_power.hip, profiles/r2/attn_m16/mfma_power_16x16x32.log)
 MFMA_LOOP_BF16_TFLOPS = 1880.3
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r5", "bench_pmc", "pmc_self.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r6", "bench_pmc", "pmc_self.json")
 
 
 def parse():
