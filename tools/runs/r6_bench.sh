@@ -14,6 +14,6 @@ print('cpu', json.dumps(d.get('cpu_baseline')))"
 if [ "${PROF:-1}" = 1 ]; then
   cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
   timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_prof.json 2> $O/bench_prof.err || { tail -20 $O/bench_prof.err; exit 1; }
-  find $O/prof -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $O/bench_kernel_stats.csv
-  head -12 $O/bench_kernel_stats.csv | cut -c1-200
+  python3 tools/prof_db_stats.py $(find $O/prof -name "*.db" | head -1) $O/bench_kernel_stats.csv
+  head -8 $O/bench_kernel_stats.csv | cut -c1-160
 fi
