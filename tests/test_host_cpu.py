@@ -22,7 +22,7 @@ def test_library_exports_every_header_symbol():
     hdr = open(__graft_entry__.ROOT + "/include/cp25.h").read()
     # every function declaration at column 0, whatever its return type (int, int64_t, size_t, const char*)
     declared = sorted(set(re.findall(r"^(?:const\s+)?[A-Za-z_]\w*\s*\**\s*(cp25_\w+)\(", hdr, re.M)))
-    assert len(declared) >= 45 and "cp25_gemm_f32_workspace_floats" in declared and "cp25_attn_kernel" in declared
+    assert len(declared) >= 48 and "cp25_gemm_epi_t" in declared and "cp25_gemm_f32_workspace_floats" in declared and "cp25_attn_kernel" in declared
     lib = _native.load_library()
     for name in declared:
         assert hasattr(lib, name), name
