@@ -765,9 +765,9 @@ class MinimalV1LVGDiT:
         if cfg.action_dim:
             if action is None:
                 raise ValueError("this action-conditioned net needs `action`")
-            e_d, e_3d = self.action_embedding(action, B, T)
-            sincos = sincos + e_d.reshape(B * T, D)
-            lora = lora + e_3d.reshape(B * T, 3 * D)
+            e_d, e_3d = self.action_embedding(action, B, T)  # [B, T or 1, *]: broadcast over the frames
+            sincos = (sincos.view(B, T, D) + e_d).reshape(B * T, D)
+            lora = (lora.view(B, T, 3 * D) + e_3d).reshape(B * T, 3 * D)
         elif action is not None:
             raise ValueError("`action` given to a net without action embedders")
         xf = sincos.float()

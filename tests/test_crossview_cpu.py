@@ -67,3 +67,35 @@ def test_crossview_neighbours():
     assert net._cross_view_neighbours(geo2, torch.tensor([0, 2])) == [[1], [0]]
     # input views (1, 2): view 1's only neighbour (0) is absent -> none; view 2's (0, 1) -> id 1 (position 0)
     assert net._cross_view_neighbours(geo2, torch.tensor([1, 2])) == [[], [0]]
+
+
+@pytest.mark.parametrize("per_frame", [4, 0])
+def test_action_net_bf16_conditioning_cpu(per_frame):
+    """The bf16-conditioning path (use_wan_fp32_strategy=False) with action embeddings added per latent frame or per
+    chunk (broadcast over the frames), host path with the CPU stand-ins, against the oracle's restatement."""
+    import dataclasses
+
+    import cpu_kernels
+    from cosmos_predict2.dit import MinimalV1LVGDiT, init_state_dict
+    from cosmos_predict2.net_config import tiny_dit
+    from oracle import dit as odit
+
+    cfg = tiny_dit(num_blocks=1, action_dim=7, action_per_latent_frame=per_frame, num_action_per_chunk=12,
+                   use_wan_fp32_strategy=False)
+    sd = {"net." + k: v for k, v in init_state_dict(cfg, seed=6, zero_adaln_out=False).items()}
+    g = torch.Generator().manual_seed(2)
+    T = 4
+    x = torch.randn(1, 16, T, 8, 16, generator=g)
+    mask = torch.zeros(1, 1, T, 8, 16)
+    mask[:, :, :1] = 1
+    t = torch.tensor([[0.1] + [700.0] * (T - 1)])
+    ctx = torch.randn(1, 512, cfg.crossattn_proj_in_channels, generator=g).to(torch.bfloat16)
+    act = torch.randn(1, 12, 7, generator=g)
+    ref = odit.dit_forward(dataclasses.asdict(cfg), sd, x, t, ctx, mask, action=act)
+    with cpu_kernels.patched(), torch.no_grad():
+        net = MinimalV1LVGDiT(cfg, device="cpu")
+        net.load_state_dict(sd)
+        out = net(x.to(torch.bfloat16), t, ctx, condition_video_input_mask_B_C_T_H_W=mask, action=act)
+    rel = ((out.float() - ref).norm() / ref.norm()).item()
+    print(f"action net, bf16 conditioning, per_frame={per_frame}: rel-L2 {rel:.3e}")
+    assert rel <= 1e-2, rel
