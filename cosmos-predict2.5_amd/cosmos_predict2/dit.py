@@ -625,9 +625,10 @@ class MinimalV1LVGDiT:
             wb[:, k_in] = bias
             self._bias_w[key] = wb
             p[key + ".weight"] = wb[:, :k_in]  # one copy in HBM: the state dict's weight is now a view of wb
-        a = torch.zeros((x.shape[0], kp), dtype=BF16, device=self.device)
+        a = torch.empty((x.shape[0], kp), dtype=BF16, device=self.device)
         a[:, :k_in] = x
         a[:, k_in] = 1.0
+        a[:, k_in + 1:] = 0.0  # only the pad columns are cleared (no full-size zero fill)
         return N.gemm_epi(a, wb, epilogue=epilogue)
 
     def rope_tables(self, geo: Geometry) -> Tuple[torch.Tensor, torch.Tensor]:

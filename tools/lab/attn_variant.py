@@ -5,7 +5,8 @@ usage: python tools/lab/attn_variant.py <name> <patch>[,<patch>...]  ->  tools/l
 patches: nostore (no O stores at block boundaries), nodma (no next-block Q copy), noqread (no Q read from LDS),
 nostagger (the Q copy at tile 0 in every workgroup; correct results), rowsum_first (correct results),
 prio_b_hold, prio_static_b (wave priority forms; correct results), ahead3, ahead4 (operand ring depth;
-correct results), hotload, noload (staging-load probes), noexp, noreads (round-5 isolation builds), none
+correct results), hotload, noload (staging-load probes), noexp, noreads (round-5 isolation builds), kv_sc1, kv_nt,
+kv_sc0sc1 (the K / V DMA's cache policy, round 6; correct results), none
 DEFINES="-D..." adds compile definitions (e.g. -DCP25_ATTN_PROBE for the s_memtime probe)"""
 import os
 import subprocess
@@ -104,6 +105,11 @@ PATCHES = {
               "          v[j] = static_cast<__bf16>(e_);\n"),
              ("    const float l_tot = lsum[qh][0];\n", "    const float l_tot = group4_sum(lsum[qh][0] + lsum[qh][1]);\n"),
              ("      const float inv = 1.f / lsum[qh][0];\n", "      const float inv = 1.f / group4_sum(lsum[qh][0] + lsum[qh][1]);\n")],
+    # round 6: cache policy of the self-attention's K / V LDS-DMA (correct results): sc1 / sc0 sc1 / nt loads are
+    # L2-served and allocate no L1 line (MI355X_MICROARCH.md); K / V tiles are read once per workgroup
+    "kv_sc1": [('      asm volatile("s_mov_b32 m0, %2\\n\\ts_nop 0\\n\\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(tsrc),\n', '      asm volatile("s_mov_b32 m0, %2\\n\\ts_nop 0\\n\\tglobal_load_lds_dwordx4 %0, %1 sc1" ::"v"(off), "s"(tsrc),\n')],
+    "kv_nt": [('      asm volatile("s_mov_b32 m0, %2\\n\\ts_nop 0\\n\\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(tsrc),\n', '      asm volatile("s_mov_b32 m0, %2\\n\\ts_nop 0\\n\\tglobal_load_lds_dwordx4 %0, %1 nt" ::"v"(off), "s"(tsrc),\n')],
+    "kv_sc0sc1": [('      asm volatile("s_mov_b32 m0, %2\\n\\ts_nop 0\\n\\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(tsrc),\n', '      asm volatile("s_mov_b32 m0, %2\\n\\ts_nop 0\\n\\tglobal_load_lds_dwordx4 %0, %1 sc0 sc1" ::"v"(off), "s"(tsrc),\n')],
     "none": [],
 }
 
@@ -122,7 +128,8 @@ def main():
              "-fno-honor-nans", "-fno-slp-vectorize", "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
     flags += os.environ.get("DEFINES", "").split()  # e.g. DEFINES=-DCP25_ATTN_PROBE
     subprocess.check_call(["/opt/rocm/bin/hipcc", *flags, "-c", tmp, "-o", f"/tmp/attn_{name}.o"])
-    others = [os.path.join(OBJ, f + ".o") for f in ("dit_ops", "fp8_ops", "gemm", "unipc", "vae_attn", "vae_ops")]
+    others = [os.path.join(OBJ, f) for f in sorted(os.listdir(OBJ))
+              if f.endswith(".o") and f not in ("attn_fwd.o", "attn_w64.o")]
     out = os.path.join(ROOT, "tools", "lab", f"libcp25_{name}.so")
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out,
                            f"/tmp/attn_{name}.o", *others])
