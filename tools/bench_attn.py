@@ -102,6 +102,10 @@ def main():
     ap.add_argument("--ab", type=int, default=0,
                     help="A/B: after the timing, N more rounds alternating attn_fwd_m16 / attn_fwd_w64 launches "
                          "(iters each), reported as ms lists per form")
+    ap.add_argument("--ab-libs", default="",
+                    help="comma-separated lab builds of libcp25.so: after the timing, --ab rounds alternating the "
+                         "loaded library and these (rotating order, iters launches each), reported as ms lists per "
+                         "library, with each library's output compared bit for bit with the first's")
     ap.add_argument("--probe", type=int, default=-1,
                     help="with a -DCP25_ATTN_PROBE lab build: after the timing, one more launch records s_memtime "
                          "stamps of tiles probe .. probe + 31 in the first --probe-wg workgroups (probe_report)")
@@ -187,7 +191,7 @@ def main():
     ms = e0.elapsed_time(e1) / a.iters
     flop = 4.0 * a.B * a.H * a.L * Lk * 128
     ab = None
-    if a.ab > 0:
+    if a.ab > 0 and not a.ab_libs:
         ab = {"m16": [], "w64": []}
         prev = N.attn_self_select(0)
         for _ in range(a.ab):
@@ -201,6 +205,30 @@ def main():
                 torch.cuda.synchronize()
                 ab[key].append(round(e0.elapsed_time(e1) / a.iters, 3))
         N.attn_self_select(prev)
+    if a.ab_libs:
+        libs = {os.path.basename(a.lib) or "libcp25.so": N.load_library()}
+        for path in a.ab_libs.split(","):
+            N._lib, N._LIB_PATH = None, path
+            libs[os.path.basename(path)] = N.load_library()
+        names = list(libs)
+        ab, same, o0 = {n: [] for n in names}, {}, None
+        for r in range(max(a.ab, 1)):
+            for n in names[r % len(names):] + names[:r % len(names)]:
+                N._lib = libs[n]
+                N.attn_fwd(q, k, v, out=o, n_split=ns, norm_bounds=nb, **pre)
+                torch.cuda.synchronize()
+                if r == 0:
+                    if o0 is None:
+                        o0 = o.clone()
+                    same[n] = bool(torch.equal(o, o0))
+                e0.record(st)
+                for _ in range(a.iters):
+                    N.attn_fwd(q, k, v, out=o, n_split=ns, norm_bounds=nb, **pre)
+                e1.record(st)
+                torch.cuda.synchronize()
+                ab[n].append(round(e0.elapsed_time(e1) / a.iters, 3))
+        N._lib = libs[names[0]]
+        ab = {"ms": ab, "median": {n: sorted(v_)[len(v_) // 2] for n, v_ in ab.items()}, "bit_identical": same}
     probe = None
     if a.probe >= 0:
         import ctypes
