@@ -110,6 +110,17 @@ PATCHES = {
     "kv_sc1": [('      asm volatile("s_mov_b32 m0, %2\\n\\ts_nop 0\\n\\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(tsrc),\n', '      asm volatile("s_mov_b32 m0, %2\\n\\ts_nop 0\\n\\tglobal_load_lds_dwordx4 %0, %1 sc1" ::"v"(off), "s"(tsrc),\n')],
     "kv_nt": [('      asm volatile("s_mov_b32 m0, %2\\n\\ts_nop 0\\n\\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(tsrc),\n', '      asm volatile("s_mov_b32 m0, %2\\n\\ts_nop 0\\n\\tglobal_load_lds_dwordx4 %0, %1 nt" ::"v"(off), "s"(tsrc),\n')],
     "kv_sc0sc1": [('      asm volatile("s_mov_b32 m0, %2\\n\\ts_nop 0\\n\\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(tsrc),\n', '      asm volatile("s_mov_b32 m0, %2\\n\\ts_nop 0\\n\\tglobal_load_lds_dwordx4 %0, %1 sc0 sc1" ::"v"(off), "s"(tsrc),\n')],
+    # round 6: the pad lanes of each 288-B LDS row (2 of 18) issue no K / V load at all (exec-masked) instead of
+    # re-reading the tile's first 16 B; correct results
+    "kv_padskip": [("  int dma_off[5];             // lane source offsets of a full tile, per instruction\n",
+                    "  int dma_off[5];             // lane source offsets of a full tile, per instruction\n"
+                    "  unsigned dma_ok = 0;\n"),
+                   ("    dma_off[j] = cb < 2 * kD ? row * (int)(sl * 2) + cb : 0;\n",
+                    "    dma_off[j] = cb < 2 * kD ? row * (int)(sl * 2) + cb : 0;\n"
+                    "    dma_ok |= (cb < 2 * kD ? 1u : 0u) << j;\n"),
+                   ('      asm volatile("s_mov_b32 m0, %2\\n\\ts_nop 0\\n\\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(tsrc),\n',
+                    '      if (dma_ok >> j & 1u)\n'
+                    '      asm volatile("s_mov_b32 m0, %2\\n\\ts_nop 0\\n\\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(tsrc),\n')],
     "none": [],
 }
 

@@ -7,5 +7,5 @@ mkdir -p $O
 export PYTHONPATH=$PWD/cosmos-predict2.5_amd
 L=tools/lab
 timeout -k 10 400 python -u tools/bench_attn.py --fused --bounded --prescaled --qnorm --iters 4 --ab 6 \
-  --ab-libs $L/libcp25_none.so,$L/libcp25_kv_sc1.so,$L/libcp25_kv_nt.so,$L/libcp25_kv_sc0sc1.so > $O/ab_unit.json 2> $O/ab_unit.err || { tail -5 $O/ab_unit.err; exit 1; }
+  --ab-libs ${LIBS:-$L/libcp25_none.so,$L/libcp25_kv_sc1.so,$L/libcp25_kv_nt.so,$L/libcp25_kv_sc0sc1.so} > $O/ab_unit.json 2> $O/ab_unit.err || { tail -5 $O/ab_unit.err; exit 1; }
 cat $O/ab_unit.json
