@@ -134,3 +134,41 @@ def test_gemm_fp8_matches_dequantised(device, M, Nn, K):
     fr = torch.arange(M, device=device) // hw
     exp = _rbf(xr[:, 0].float() + _rbf(gate[0, fr].float() * out.float()))
     assert torch.equal(o2.float(), exp)
+
+
+def _tail_plan(M, Nn, cus):
+    """The persistent kernel's tail plan (gemm.hip `plan`): whole tiles, or the last round as half / quarter slices."""
+    tiles = (M + 255) // 256 * (Nn // 256)
+    P = min(4 * tiles, cus)
+    R = tiles % P
+    return "full" if R == 0 else ("quarter" if 4 * R <= P else ("half" if 2 * R <= P else "whole"))
+
+
+def test_gemm_rows_independent_of_tail_plan(device):
+    """Round 6's tail row slices (gemm.hip `plan`): a row computed in a whole tile, a half slice or a quarter slice is
+    the same MFMA chain, so every row is bit-identical whichever plan its launch's M gives it. Row prefixes of one
+    problem at M values that put the launch in each plan (full rounds only, quarter / half slices for the last round,
+    whole tiles in a partial last round), on the persistent K = 2048 kernel, plain / GELU / gated-residual epilogues."""
+    cus = torch.cuda.get_device_properties(device).multi_processor_count
+    cus = cus & ~7 if cus >= 8 else cus
+    Nn, K = 2048, 2048
+    pick = {}
+    for mt in range(cus // 8, 8 * cus // 8 + 1):  # at least one full round of tiles
+        M = mt * 256 - 37  # ragged last tile row
+        pick.setdefault(_tail_plan(M, Nn, cus), M)
+    assert set(pick) == {"full", "quarter", "half", "whole"}, pick
+    Mb = max(pick.values())
+    g = torch.Generator(device=device).manual_seed(11)
+    a = torch.randn(Mb, K, device=device, generator=g).to(torch.bfloat16)
+    w = (torch.randn(Nn, K, device=device, generator=g) * K ** -0.5).to(torch.bfloat16)
+    hw = 4096
+    gate = torch.randn(1, (Mb + hw - 1) // hw, Nn, device=device, generator=g).to(torch.bfloat16)
+    x = torch.randn(Mb, 1, Nn, device=device, generator=g).to(torch.bfloat16)
+    full = {e: N.gemm_epi(a, w, epilogue=e) for e in (N.EPI_NONE, N.EPI_GELU)}
+    full_res = N.gemm_res(a, w, x, x.stride(0), x.stride(1), gate, B=1, tok0=0, hw=hw)
+    for plan, M in sorted(pick.items(), key=lambda kv: kv[1]):
+        for e in (N.EPI_NONE, N.EPI_GELU):
+            assert torch.equal(N.gemm_epi(a[:M], w, epilogue=e), full[e][:M]), (plan, M, e)
+        r = N.gemm_res(a[:M], w, x[:M], x.stride(0), x.stride(1), gate, B=1, tok0=0, hw=hw)
+        assert torch.equal(r, full_res[:M]), (plan, M, "res")
+    print(f"tail plans on {cus} CUs: {pick}")
