@@ -461,8 +461,8 @@ int cp25_vae_attn(const void* q, int64_t ldq, int64_t fq, const void* k, int64_t
 int cp25_softmax_rows(const float* s, int64_t rows, int cols, int64_t ld_s, float scale, void* p, int64_t ld_p,
                       hipStream_t stream);
 
-/* fp8 activation operand of the DiT's fp8 linear layers (config 5's "fp8 MFMA"; the GEMM is hipBLASLt's
- * fp8 kernel via torch._scaled_mm). Per row m of x [n_rows, k] bf16 (contiguous, k in {512, 1024, 1536,
+/* fp8 activation operand of the DiT's fp8 linear layers (config 5's "fp8 MFMA"; the GEMM is cp25_gemm_fp8 /
+ * cp25_gemm_fp8_res, hand-written; torch._scaled_mm is only the tests' reference). Per row m of x [n_rows, k] bf16 (contiguous, k in {512, 1024, 1536,
  * 2048, 3072, 4096, 5120, 6144, 8192, 20480}): scale[m] = max|x[m, :]| / 448 and q[m, :] = fp8_e4m3(x[m, :] * 448 / max|x[m, :]|)
  * (OCP E4M3, round to nearest even, saturated), so x ~= q * scale; an all-zero row gives q = 0, scale 0.
  * cp25_gelu_quant_fp8 quantises GELU(x) rounded to bf16 (Abramowitz-Stegun 7.1.26 erfc: within ~1 bf16 ulp
