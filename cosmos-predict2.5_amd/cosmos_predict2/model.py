@@ -57,6 +57,9 @@ class Video2WorldModelRectifiedFlow:
         self.tokenizer = tokenizer
         self.sample_scheduler = FlowUniPCMultistepScheduler(num_train_timesteps=1000, shift=1)
         self.cp_group = None
+        # replay each trajectory's DiT forward from a HIP graph after its first evaluation (SamplingRun; one GPU only):
+        # for launch-bound shapes (config 5's 13-frame chunks), where the host's launch rate leaves the device idle
+        self.hip_graph = False
 
     # ------------------------------------------------------------------ plumbing
     def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
@@ -258,13 +261,21 @@ class SamplingRun:
         self.ctx = None if net_fn is not None else model.net.prepare_context(torch.cat([ctx_cond, ctx_uncond], 0))
         self.mode = 0 if (cfg_mode or model.config.cfg_mode) == "video2world" else 1
         self.guidance = guidance
-        self.action, self.view_indices = action, view_indices
+        # on the device once (a per-evaluation host copy would also be a pageable copy inside a HIP graph capture)
+        self.action = None if action is None else action.to(dev)
+        self.view_indices = view_indices
         self._sched_args = dict(num_inference_steps=num_steps, device=dev, shift=shift,
                                 use_kerras_sigma=model.config.use_kerras_sigma_at_inference)
         # the run's own solver (configured like the model's sample_scheduler): its UniPC history must not be shared
         # with another live run, nor with a sample_latents call made while this run is alive
         base = model.sample_scheduler
         self.sched = FlowUniPCMultistepScheduler(base.num_train_timesteps, base.solver_order, base.config_shift)
+        # HIP graph of the DiT forward (model.hip_graph): captured at the second evaluation, after the first one ran
+        # eagerly and built every lazily made buffer (RoPE tables, bf16 weight copies), then replayed on static copies
+        # of the two inputs that change per evaluation (patch rows, timesteps); the context, the action and every
+        # weight stay the tensors the graph recorded. Not with CP (the K/V gathers run on their own streams).
+        self._graphable = bool(getattr(model, "hip_graph", False)) and net_fn is None and world == 1
+        self._graph = None
         self.restart()
 
     def restart(self) -> None:
@@ -296,8 +307,26 @@ class SamplingRun:
         if self.net_fn is None:
             # one t row expanded over the CFG pair, one action: the entries differ only in the text context
             shared = self.action is None or self.action.shape[0] == 1
-            net_out = m.net.forward_tokens(rows.view(geo.n_tok, 1, -1), t_B_T, self.ctx, geo, action=self.action,
-                                           view_indices=self.view_indices, shared_batch=shared, rows_k128=True)
+
+            def forward(rows_, t_):
+                return m.net.forward_tokens(rows_, t_, self.ctx, geo, action=self.action,
+                                            view_indices=self.view_indices, shared_batch=shared, rows_k128=True)
+            if self._graphable and self.i >= 1:
+                # rows is the [n, 72] view of patchify's zero-padded [n, 128] buffer (rows_k128): the static copy
+                # keeps that layout, pad columns included
+                padded = torch.as_strided(rows, (rows.shape[0], rows.stride(0)), (rows.stride(0), 1))
+                if self._graph is None:
+                    self._g_buf, self._g_t = padded.clone(), t_B_T.clone()
+                    self._g_rows = self._g_buf[:, :rows.shape[1]].view(geo.n_tok, 1, -1)
+                    self._graph = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(self._graph):
+                        self._g_out = forward(self._g_rows, self._g_t)
+                self._g_buf.copy_(padded)
+                self._g_t.copy_(t_B_T)
+                self._graph.replay()
+                net_out = self._g_out
+            else:
+                net_out = forward(rows.view(geo.n_tok, 1, -1), t_B_T)
         else:
             net_out = self.net_fn(rows.view(geo.n_tok, 1, -1), t_B_T, geo)
         v = N.cfg_velocity(net_out, self.noise, self.gtp, self.kmask, self.guidance, self.mode,

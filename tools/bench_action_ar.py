@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--chunk-size", type=int, default=12)
     ap.add_argument("--linear-precision", default="bf16", choices=("bf16", "fp8"))
     ap.add_argument("--attention-precision", default="bf16", choices=("bf16", "fp8qk", "fp8"))
+    ap.add_argument("--hip-graph", action="store_true",
+                    help="replay each chunk's DiT forward from a HIP graph after its first evaluation (model.hip_graph)")
     ap.add_argument("--block-gemm", default="own", choices=("own", "lib"),
                     help="block projections on the hand-written GEMMs (default) or the library (A/B)")
     a = ap.parse_args()
@@ -40,6 +42,7 @@ def main():
         sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
         from library_gemm_net import use_library_gemms
         use_library_gemms(inf.pipe.model.net)
+    inf.pipe.model.hip_graph = a.hip_graph
     adim = inf.pipe.model.net.cfg.action_dim
     rng = np.random.RandomState(0)
     img = rng.randint(0, 256, size=(h, w, 3), dtype=np.uint8)
@@ -54,7 +57,7 @@ def main():
     assert video.shape == (a.frames, h, w, 3), video.shape
     print(json.dumps({"workload": f"action-conditioned AR {a.frames}f at {h}x{w}, {n_chunks} chunks of "
                                   f"{a.chunk_size + 1} frames, {a.num_steps} UniPC steps, CFG 7",
-                      "linear_precision": a.linear_precision, "block_gemm": a.block_gemm,
+                      "linear_precision": a.linear_precision, "block_gemm": a.block_gemm, "hip_graph": a.hip_graph,
                       "attention_precision": a.attention_precision, "n_gpus": 1, "seconds": dt,
                       "frames_per_s": a.frames / dt, "s_per_chunk": dt / n_chunks}), flush=True)
 
