@@ -107,6 +107,17 @@ def get_action_sequence_from_states(data: dict, fps_downsample_ratio: int = 1, u
 
 
 # ----------------------------------------------------------------------------- generation loop
+def conditioning_video(img: np.ndarray, n_frames: int) -> torch.Tensor:
+    """uint8 [1, 3, n_frames, H, W]: frame 0 the uint8 image [H, W, 3], the rest zeros. The reference
+    (cosmos_predict2/action_conditioned.py:326-331) builds it as to_tensor (fp32 / 255), zero frames, then
+    `(vid * 255.0).to(torch.uint8)`; that fp32 round trip returns every uint8 value unchanged, so the uint8 frame is
+    used directly (no fp32 video on the host: ~30 ms per chunk at 480x640)."""
+    H, W, _ = img.shape
+    vid = torch.zeros(1, 3, n_frames, H, W, dtype=torch.uint8)
+    vid[0, :, 0] = torch.from_numpy(np.ascontiguousarray(img)).permute(2, 0, 1)
+    return vid
+
+
 class ActionConditionedInference:
     """The reference's action-conditioned `inference()` chunk loop over one trajectory."""
 
@@ -130,9 +141,9 @@ class ActionConditionedInference:
             if a.shape[0] != chunk_size:  # zero-pad an incomplete last chunk
                 a = np.concatenate([a, np.zeros((chunk_size - a.shape[0],) + a.shape[1:], a.dtype)], 0)
             n_frames = chunk_size + 1
-            x = torch.from_numpy(np.ascontiguousarray(img)).permute(2, 0, 1).float() / 255.0  # to_tensor
-            vid = torch.cat([x[None], torch.zeros_like(x[None]).repeat(n_frames - 1, 1, 1, 1)], 0)
-            vid = (vid * 255.0).to(torch.uint8).unsqueeze(0).permute(0, 2, 1, 3, 4)  # [1, C, T, H, W]
+            # the reference's to_tensor (/ 255) -> zero frames -> * 255 -> uint8 round trip is the identity on every
+            # uint8 value in fp32 (tests/test_action_cpu.py), so the uint8 frame goes in as it is: [1, C, T, H, W]
+            vid = conditioning_video(img, n_frames)
             video = self.pipe.generate_vid2world(prompt, vid, guidance=guidance, num_video_frames=n_frames,
                                                  num_latent_conditional_frames=num_latent_conditional_frames,
                                                  resolution=f"{H},{W}", seed=i, negative_prompt=negative_prompt,
