@@ -21,6 +21,9 @@ constexpr int kThreads = kWaves * 64;
 // contract guard below poisons a row whose sum overflows. bf16 P has the fp32 exponent range.
 constexpr float kTop = 96.f;        // zero / fixed shift: largest exponent a term may reach
 constexpr float kMaxBound = 98.f;   // fixed shift: largest score bound b (smallest row-max term 2^(96 - 2 b) >= 2^-100)
+constexpr float kWhole = 63.f;      // fixed shift, whole-bound form: a row with b_row <= 63 is shifted by floor(b_row), so
+                                    // P <= 2 and its largest term >= 2^(-2 b_row) >= 2^-126 (round 6: small P runs the
+                                    // power-limited loop faster, tools/lab/ab_shift_power.py)
 constexpr float kTopF8 = 60.f;      // fp8 Q K^T form: P = exp2(S) unshifted for bound products up to this
 constexpr float kLazy = 24.f;       // online max: rescale only when a row max exceeds the shift by more (P <= 2^24)
 

@@ -10,7 +10,8 @@
 //                 K/V 64-key tiles double-buffered in padded LDS rows, counted-lgkmcnt operand ring, row sums by
 //                 MFMA, XCD-aware grid. The softmax shift of a query row enters as the initial C of its Q K^T MFMA
 //                 chains, so P = exp2(S) needs no per-score VALU beyond the exp (prescaled q). The shift is either
-//                 fixed from a norm bound (b_row = |q_row| max|k| <= 98: shift max(b_row - 96, 0), no max at all) or
+//                 fixed from a norm bound (b_row = |q_row| max|k| <= 98: shift floor(b_row) where b_row <= 63, else
+//                 max(b_row - 96, 0); no max at all) or
 //                 an online row max with lazy rescale (any data; per wave, decided at the kernel start).
 //   attn_fwd_f8   the config-5 fp8 option (no reference counterpart): Q K^T on v_mfma_f32_32x32x64_f8f6f4 over e4m3
 //                 q / k, and with kF8 = 3 also P.V on e5m2 P (made without exp2) and e4m3 V^T tiles.
@@ -51,7 +52,9 @@ using namespace cp25attn;
 // the fp32 / bf16 range. With a pre-scaled q (rows carry softmax_scale * log2 e) the shift is the initial C of the
 // row's Q K^T chains, so S arrives already shifted:
 //   zero   (pre-scaled q, bound product b <= 96): no shift; terms in [2^-b, 2^b];
-//   fixed  (b <= 98): shift max(b_row - 96, 0) from the row's own |q_row|; the row's largest term >= 2^-100;
+//   fixed  (b <= 98): from the row's own |q_row|: shift floor(b_row) if b_row <= 63 (the whole bound: P <= 2, the
+//          row's largest term >= 2^-126; the host's choice for self-attention with b <= 63, round 6), else
+//          max(b_row - 96, 0) (the row's largest term >= 2^-100);
 //   online (larger or unknown bounds): tile 0 sets the shift to the row max; a later tile rescales O and the row sum
 //          (and moves the shift) only for a row whose max exceeds the shift by more than kLazy (24), so P <= 2^24 and
 //          the row's largest term >= 1. Per tile: 16 v_max3 per lane and one ballot; the row reduction (two row swaps)
@@ -420,7 +423,10 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
           const float x = static_cast<float>(qf[qh][s][e]);
           qq = fmaf(x, x, qq);
         }
-      m_run[qh] = fmaxf(sqrtf(group4_sum(qq)) * a.kbound * cs - kTop, 0.f);
+      // b_row = |q_row| max|k| bounds every score of the row (log2 units). Whole-bound form (b_row <= kWhole): shift
+      // floor(b_row), P <= 2; else the top of the window, max(b_row - 96, 0)
+      const float b_row = sqrtf(group4_sum(qq)) * a.kbound * cs;
+      m_run[qh] = b_row <= kWhole ? floorf(b_row) : fmaxf(b_row - kTop, 0.f);
     }
   }
   f32x4 minit[2];  // kPre: -shift, the Q K^T chains' initial C
@@ -1343,10 +1349,15 @@ int plan_split(int B, int H, int Lq, int Lk) {
 }
 
 // The m16 softmax-shift mode for these bounds (the bound product in log2 units; |q_row| <= q_norm_bound): 1 zero
-// shift (pre-scaled q, product <= 96), 0 fixed per-row shift (product <= 98), 2 online max (larger or unknown)
-int m16_mode(float q_norm_bound, float k_norm_bound, float scale_log2, bool prescaled) {
+// shift (pre-scaled q, product <= 96), 0 fixed per-row shift (product <= 98), 2 online max (larger or unknown).
+// whole_ok (long-key self-attention launches, round 6): a product <= kWhole takes the fixed mode, whose rows then
+// shift by their whole bound (P <= 2): measured 0.8 % faster than the zero shift at the metric launch, the same cycles
+// at a higher power-limited clock (profiles/r6/shift_power/). Short-key launches keep the zero shift (the persistent
+// cross-attention has no fixed mode).
+int m16_mode(float q_norm_bound, float k_norm_bound, float scale_log2, bool prescaled, bool whole_ok = false) {
   const double bb = (double)q_norm_bound * k_norm_bound * (prescaled ? 1.0 : scale_log2);
   if (!(q_norm_bound > 0.f && k_norm_bound > 0.f) || bb > kMaxBound) return 2;
+  if (whole_ok && bb <= kWhole) return 0;
   return prescaled && bb <= kTop ? 1 : 0;
 }
 
@@ -1491,12 +1502,12 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
   } else if (fp8qk) {
     hipLaunchKernelGGL((xk ? attn_fwd_f8<1, 1> : attn_fwd_f8<0, 1>), dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
   } else {
-    const int mode = m16_mode(q_norm_bound, k_norm_bound, a.scale_log2, prescaled);
+    const int mode = m16_mode(q_norm_bound, k_norm_bound, a.scale_log2, prescaled, !xk);
     void (*kern)(AttnArgs) = nullptr;
     void (*kern_tail)(AttnArgs) = nullptr;  // the tail segments' symbol (plan_tail: self-attention shapes only)
     int64_t grid = nwg;
     int threads = kThreads;
-    if (prescaled && kslots && mode != 1) {
+    if (prescaled && kslots && m16_mode(q_norm_bound, k_norm_bound, 1.f, true) != 1) {
       // the gated pair: blocks whose data-tight bound allows it run the zero-shift loop, the others the online max
       hipLaunchKernelGGL((xk ? attn_fwd_m16<1, true, 1, false, 1> : attn_fwd_m16<0, true, 1, false, 1>),
                          dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
@@ -1696,5 +1707,5 @@ extern "C" const char* cp25_attn_kernel(int Lk, float softmax_scale, float q_nor
        {"attn_fwd_m16<cross, prescaled, fixed shift>", "attn_fwd_m16<cross, prescaled, zero shift>",
         "attn_fwd_m16<cross, prescaled, online max>"}}};
   const float sl = prescaled ? 1.f : softmax_scale * 1.4426950408889634f;
-  return names[Lk <= 4096][prescaled != 0][m16_mode(q_norm_bound, k_norm_bound, sl, prescaled != 0)];
+  return names[Lk <= 4096][prescaled != 0][m16_mode(q_norm_bound, k_norm_bound, sl, prescaled != 0, Lk > 4096)];
 }

@@ -113,4 +113,6 @@ def test_gated_pair_without_slots_is_online(device):
 
 def test_gated_kernel_name(device):
     assert "gated" in N.attn_kernel_name(109120, norm_bounds=(4.4, 34.6), prescaled=2)
-    assert "zero shift" in N.attn_kernel_name(109120, norm_bounds=(1.5, 11.6), prescaled=2)
+    # inside the zero-shift window no gate: a long-key launch with a product <= 63 takes the whole-bound fixed shift
+    assert "fixed shift" in N.attn_kernel_name(109120, norm_bounds=(1.5, 11.6), prescaled=2)
+    assert "zero shift" in N.attn_kernel_name(109120, norm_bounds=(7.0, 11.6), prescaled=2)

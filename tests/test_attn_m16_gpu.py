@@ -63,9 +63,14 @@ def test_m16_modes_match_fp32(device, B, H, Lq, Lk, n_split, prescaled):
         ref = ref_attention(qin, k, v, 1.0 / LOG2E)
         base = dict(prescaled=True, n_split=n_split)
         qb = qin.float().norm(dim=-1).max().item() * 1.01
-        # zero shift (product <= 96), fixed shift (product in (96, 98]: inflated q bound), online
-        modes = {"zero": dict(base, norm_bounds=(qb, kn)), "fixed": dict(base, norm_bounds=(97.0 / kn, kn)),
-                 "online": dict(base)}
+        # the data's bounds (product <= 63: the whole-bound fixed shift for long keys, the zero shift for short ones),
+        # zero shift (product 80: inflated q bound), fixed shift (product in (96, 98]), online
+        modes = {"tight": dict(base, norm_bounds=(qb, kn)), "zero": dict(base, norm_bounds=(max(qb, 80.0 / kn), kn)),
+                 "fixed": dict(base, norm_bounds=(97.0 / kn, kn)), "online": dict(base)}
+        assert qb * kn <= 63.0
+        exp = "fixed shift" if Lk > 4096 else "zero shift"
+        assert exp in N.attn_kernel_name(Lk, norm_bounds=(qb, kn), prescaled=True)
+        assert "zero shift" in N.attn_kernel_name(Lk, norm_bounds=(max(qb, 80.0 / kn), kn), prescaled=True)
     else:
         qin = q
         ref = ref_attention(q, k, v, scale)
@@ -215,6 +220,27 @@ def test_m16_zero_shift_top_of_window_long_keys(device):
     q, k = q.to(device, torch.bfloat16), k.to(device, torch.bfloat16)
     assert N.attn_kernel_name(Lk, None, (8.0, 12.0), True).endswith("zero shift>")
     o = N.attn_fwd(q, k, v, norm_bounds=(8.0, 12.0), prescaled=True)
+    torch.cuda.synchronize()
+    assert torch.isfinite(o.float()).all()
+    mean_v = v.float().mean(1)[0, 0]
+    assert rel_l2(o[0, :, 0], mean_v.expand(Lq, 128)) <= 2 ** -8
+
+
+@pytest.mark.parametrize("sign", [1.0, -1.0])
+def test_m16_whole_bound_shift_edges(device, sign):
+    """The whole-bound fixed shift (round 6: long-key launches whose bound product is <= kWhole = 63 shift each row by
+    floor(b_row)): every score at +b (the top, P = 2^(b - floor(b)) <= 2) or at -b (the bottom: P = 2^(-2 b + ...) at
+    b = 62.5, down to 2^-125, still a normal bf16 / fp32), over 8192 keys. All terms equal, so O = mean(v) up to the
+    bf16 output rounding."""
+    Lq, Lk = 256, 8192
+    g = torch.Generator(device="cpu").manual_seed(14)
+    q = torch.zeros(1, Lq, 1, 128)
+    k = torch.zeros(1, Lk, 1, 128)
+    q[..., 0], k[..., 0] = 5.0, sign * 12.5  # bf16-exact; pre-scaled score +-62.5 (log2 units)
+    v = (torch.randn(1, Lk, 1, 128, generator=g) * 10.0).to(device, torch.bfloat16)
+    q, k = q.to(device, torch.bfloat16), k.to(device, torch.bfloat16)
+    assert N.attn_kernel_name(Lk, None, (5.0, 12.5), True).endswith("fixed shift>")
+    o = N.attn_fwd(q, k, v, norm_bounds=(5.0, 12.5), prescaled=True)
     torch.cuda.synchronize()
     assert torch.isfinite(o.float()).all()
     mean_v = v.float().mean(1)[0, 0]

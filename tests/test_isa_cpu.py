@@ -75,6 +75,19 @@ def test_self_attention_loop_shape():
     assert r["nops"] <= 64, r["nops"]
 
 
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="hipcc not installed")
+def test_self_attention_fixed_shift_loop_shape():
+    """The fixed-shift instantiation, the bench's kernel since round 6 (the whole-bound shift, m16_mode whole_ok): its
+    per-row shift rides as the Q K^T chains' initial C, 8 more live VGPRs at the 256 cap. Its in-loop scratch is
+    confined to cold branches (the ragged last key tile's DMA offsets and the contract guard): at most 8 such
+    instructions, none in the MFMA / softmax phases' straight-line code; hazard pads as in the zero-shift loop."""
+    rep = isa_check.check(os.path.join(CSRC, "attn_fwd.hip"), "attn_fwd_m16ILi0ELb1ELi0ELb0ELi0ELi0EE")
+    (r,) = rep.values()
+    assert r["inloop_scratch"] <= 8, r["inloop_scratch"]
+    assert r["inloop_nops"] <= 16, r["inloop_nops"]
+    assert r["nops"] <= 64, r["nops"]
+
+
 _SYNTH = """_Zk:
 \tds_read_b128 v[0:3], v10
 \ts_cbranch_scc1 .LBB0_2

@@ -121,6 +121,11 @@ PATCHES = {
                    ('      asm volatile("s_mov_b32 m0, %2\\n\\ts_nop 0\\n\\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(tsrc),\n',
                     '      if (dma_ok >> j & 1u)\n'
                     '      asm volatile("s_mov_b32 m0, %2\\n\\ts_nop 0\\n\\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(tsrc),\n')],
+    # round 6: the fixed-shift mode (kMode 0) with the shift the row's whole bound, floor(|q_row| kbound), instead of
+    # max(b_row - 96, 0): P <= 2 like the online max, and an integer shift, so outputs stay bit-identical to the zero-
+    # shift loop (P scaled by an exact power of two). Lab probe of whether P's magnitude moves the power-limited clock
+    "dshift": [("      m_run[qh] = fmaxf(sqrtf(group4_sum(qq)) * a.kbound * cs - kTop, 0.f);\n",
+                "      m_run[qh] = floorf(sqrtf(group4_sum(qq)) * a.kbound * cs);\n")],
     "none": [],
 }
 
