@@ -63,9 +63,9 @@ def parse():
     ap.add_argument("--norm-weights", default="",
                     help="lo,hi: every q/k RMSNorm weight uniform in [lo, hi] (seeded) instead of the init's ones -- the "
                          "attention then runs the form a trained checkpoint gets (the report names it)")
-    ap.add_argument("--data-tight-k-bound", action="store_true",
-                    help="with --norm-weights: the gated zero-shift / online attention pair on the measured max |k| "
-                         "(dit.data_tight_k_bound; off by default)")
+    ap.add_argument("--no-data-tight-k-bound", action="store_true",
+                    help="trained-size norm weights: the online max instead of the gated pair on the measured key "
+                         "bound (dit.data_tight_k_bound, on by default since round 6)")
     ap.add_argument("--no-whole-video", action="store_true",
                     help="skip the end-to-end video (value is then the per-evaluation model; for quick A/B runs)")
     ap.add_argument("--no-cfg-share", action="store_true",
@@ -175,7 +175,7 @@ def main():
                                 linear_precision=a.linear_precision, attention_precision=a.attention_precision)
     model = pipe.model
     model.net.share_cfg_block0 = not a.no_cfg_share
-    model.net.data_tight_k_bound = a.data_tight_k_bound
+    model.net.data_tight_k_bound = not a.no_data_tight_k_bound
     if a.norm_weights:
         lo, hi = (float(x) for x in a.norm_weights.split(","))
         gw = torch.Generator(device=dev).manual_seed(7)

@@ -278,7 +278,7 @@ def attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: Optional[to
     are then only shape references. fp8_v=(v8t, v_amax) (with fp8_qk; from cast_v_fp8t(v)): P.V on e5m2 P and
     e4m3 V too (cp25_attn_fwd_prescaled_fp8; needs 1.13 x the bound product <= 30); v is then only a shape
     reference. k_norm_slots (with prescaled, bf16): the float32 [64, 32] slots head_rmsnorm_rope(norm_max=...) filled
-    for k, a data-tight key bound (cp25_attn_fwd_prescaled_kslots: blocks whose bound allows it run the zero-shift
+    for k, a data-tight key bound (cp25_attn_fwd_prescaled_kslots: blocks whose bound allows it run the fixed-shift
     loop even when norm_bounds do not).
     q_norm=dict(weight=w [128] bf16, cos=None|[Lq, 64] fp32, sin=..., eps=1e-6, out_scale=c) (with prescaled, bf16
     attention): q holds the raw projection and the kernel applies head_rmsnorm_rope(weight, cos, sin, out_scale)'s

@@ -274,17 +274,19 @@ class MinimalV1LVGDiT:
         # the CFG pair's shared block-0 prefix runs once (see _blocks); False: every entry computes it
         self.share_cfg_block0 = True
         # single-GPU self-attention with weight-based norm bounds past the zero-shift window (trained q/k norm weights):
-        # True: the k RMSNorm kernel measures max |k| (64 device slots) and the attention runs the gated pair, the
-        # zero-shift loop for every 256-query block whose data-tight bound allows it (cp25_attn_fwd_prescaled_kslots).
-        # Off by default since round 4: with V staged by LDS-DMA the online-max form runs within 0.5 % of the zero-shift
-        # loop (profiles/r4/attn_dma, r4ab_*), and without the gate a row's arithmetic never depends on its 256-row
-        # block or on the other CFG entry's keys, so context-parallel shards stay bit-identical to CP = 1 with any
-        # checkpoint (tests/test_cp_gpu.py "nw_weight") -- under CP25_ATTN_SPLIT=1 only: by default the attention's
-        # tail split (cp25_attn_tail_workspace_bytes) runs the query blocks of a launch's last partial round as
-        # key-range splits, and which blocks those are depends on the launch's workgroup count mod the CU count, so
-        # it differs between CP = 1 and a shard (and between GPUs with different CU counts); those rows then differ
-        # from the unsplit ones by rounding (the same distance from fp32, tests/test_attn_m16_gpu.py)
-        self.data_tight_k_bound = False
+        # True (default since round 6): the k RMSNorm kernel measures max |k| (64 device slots) and the attention runs
+        # the gated pair, the fixed-shift loop on that measured bound for every 256-query block it allows (<= 110 in
+        # log2 units; small P, no running max), the online max for the rest (cp25_attn_fwd_prescaled_kslots): -0.83 %
+        # per sampler evaluation against the online max with norm weights in [0.5, 3], the k norm's separate max-|k|
+        # pass included (profiles/r6/shift_power/ab_in_dit_trained.json). False: the online max, whose rows never
+        # depend on their 256-row block or on the other CFG entry's keys. Context-parallel shards always take the
+        # weight bounds (the CP path does not read this flag), so they stay bit-identical to a CP = 1 run with it off
+        # (tests/test_cp_gpu.py "nw_weight") -- under CP25_ATTN_SPLIT=1 only: by default the attention's tail split
+        # (cp25_attn_tail_workspace_bytes) runs the query blocks of a launch's last partial round as key-range splits,
+        # and which blocks those are depends on the launch's workgroup count mod the CU count, so it differs between
+        # CP = 1 and a shard (and between GPUs with different CU counts); those rows then differ from the unsplit ones by
+        # rounding (the same distance from fp32, tests/test_attn_m16_gpu.py)
+        self.data_tight_k_bound = True
         # the self-attention normalises its own q (cp25_attn_fwd_prescaled_qnorm: head_rmsnorm_rope's arithmetic on
         # the Q fragments as they load, bit-identical, no separate pass over q in HBM); prescaled bf16 form only
         self.fused_q_norm = True

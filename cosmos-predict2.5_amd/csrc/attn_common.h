@@ -23,7 +23,10 @@ constexpr float kTop = 96.f;        // zero / fixed shift: largest exponent a te
 constexpr float kMaxBound = 98.f;   // fixed shift: largest score bound b (smallest row-max term 2^(96 - 2 b) >= 2^-100)
 constexpr float kWhole = 63.f;      // fixed shift, whole-bound form: a row with b_row <= 63 is shifted by floor(b_row), so
                                     // P <= 2 and its largest term >= 2^(-2 b_row) >= 2^-126 (round 6: small P runs the
-                                    // power-limited loop faster, tools/lab/ab_shift_power.py)
+                                    // power-limited loop faster, tools/lab/ab_shift_power.py); a row past 63 by
+                                    // floor(126 - b_row): P <= 2^(2 b_row - 125), its largest term still >= 2^-126
+constexpr float kGateFixed = 110.f; // gated pair: a block whose data-tight bound is <= 110 runs the fixed shift, whose
+                                    // rows then keep P <= 2^(2 * 110 - 125) = 2^95 (inside the zero-shift window's 2^96)
 constexpr float kTopF8 = 60.f;      // fp8 Q K^T form: P = exp2(S) unshifted for bound products up to this
 constexpr float kLazy = 24.f;       // online max: rescale only when a row max exceeds the shift by more (P <= 2^24)
 

@@ -103,10 +103,12 @@ constexpr int kLdsP = kLds16 + kWaves * kQSlot;     // 141312
 
 // kMode: 0 fixed shift, 1 fixed shift known to be 0 (pre-scaled q, bound product <= 96: no initial C), 2 online.
 // kGate (cp25_attn_fwd_prescaled_kslots: a data-tight key bound in device memory, the max |k| the producing RMSNorm
-// kernel measured): the same grid is launched twice, kGate 1 with kMode 1 and kGate 2 with kMode 2; a workgroup
-// whose query block's bound max|q_row| max|k| is <= 96 runs in the first launch (no shift, the fast loop) and exits
-// at once in the second, any other runs in the second (online max). Each block's arithmetic is exactly that of its
-// mode; which mode a row gets depends on the other rows of its 256-row block.
+// kernel measured): the same grid is launched twice, kGate 1 with kMode 0 and kGate 2 with kMode 2; a workgroup
+// whose query block's bound max|q_row| max|k| is <= kGateFixed (110) runs in the first launch (the fixed shift from
+// the measured key bound: small P, no max; round 6, it was the zero shift) and exits at once in the second, any other
+// runs in the second (online max). Each block's arithmetic is exactly that of its mode (the first launch's: a
+// fixed-shift launch whose key bound is the measured one x 1.001); which mode a row gets depends on the other rows of
+// its 256-row block.
 // kTail = 1: the same code as a separate symbol, launched for the tail-split segments, so profiles separate the main
 // grid from the segments that finish its last partial round.
 template <int kKind, bool kPre, int kMode, bool kPersist = false, int kGate = 0, int kTail = 0>
@@ -366,8 +368,9 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
     }
   }
 
+  float gate_kbound = a.kbound;  // (the gated pair's first launch: the data-tight key bound from the slots)
   if constexpr (kGate != 0) {
-    static_assert(kPre && !kPersist && ((kGate == 1 && kMode == 1) || (kGate == 2 && kMode == 2)), "gated pair");
+    static_assert(kPre && !kPersist && ((kGate == 1 && kMode == 0) || (kGate == 2 && kMode == 2)), "gated pair");
     __shared__ float gate_max[kWaves];
     float km = lane < a.n_kslots ? a.kslots[32 * lane] : 0.f;  // max |k| over all keys (slots 128 B apart)
     float qm = 0.f;                                      // max |q_row| over this wave's rows
@@ -393,8 +396,9 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) qm = fmaxf(qm, gate_max[w]);
     // bound product with a 1e-3 margin (fp32 sums of the scores and of the norms); no slots written: online
-    const bool zero_ok = km > 0.f && qm * km * 1.001f <= kTop;
-    if (zero_ok != (kGate == 1)) {  // uniform over the workgroup
+    const bool fixed_ok = km > 0.f && qm * km * 1.001f <= kGateFixed;
+    gate_kbound = km * 1.001f;  // the fixed-shift rows' key bound: the measured one
+    if (fixed_ok != (kGate == 1)) {  // uniform over the workgroup
       if constexpr (kDmaK) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup
       return;
     }
@@ -424,9 +428,9 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
           qq = fmaf(x, x, qq);
         }
       // b_row = |q_row| max|k| bounds every score of the row (log2 units). Whole-bound form (b_row <= kWhole): shift
-      // floor(b_row), P <= 2; else the top of the window, max(b_row - 96, 0)
-      const float b_row = sqrtf(group4_sum(qq)) * a.kbound * cs;
-      m_run[qh] = b_row <= kWhole ? floorf(b_row) : fmaxf(b_row - kTop, 0.f);
+      // floor(b_row), P <= 2; past it floor(126 - b_row) (P <= 2^(2 b_row - 125), the largest term >= 2^-126)
+      const float b_row = sqrtf(group4_sum(qq)) * gate_kbound * cs;
+      m_run[qh] = floorf(b_row <= kWhole ? b_row : 126.f - b_row);
     }
   }
   f32x4 minit[2];  // kPre: -shift, the Q K^T chains' initial C
@@ -1508,8 +1512,9 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
     int64_t grid = nwg;
     int threads = kThreads;
     if (prescaled && kslots && m16_mode(q_norm_bound, k_norm_bound, 1.f, true) != 1) {
-      // the gated pair: blocks whose data-tight bound allows it run the zero-shift loop, the others the online max
-      hipLaunchKernelGGL((xk ? attn_fwd_m16<1, true, 1, false, 1> : attn_fwd_m16<0, true, 1, false, 1>),
+      // the gated pair: blocks whose data-tight bound allows it (<= kGateFixed) run the fixed-shift loop with the
+      // measured key bound, the others the online max
+      hipLaunchKernelGGL((xk ? attn_fwd_m16<1, true, 0, false, 1> : attn_fwd_m16<0, true, 0, false, 1>),
                          dim3((unsigned)nwg), dim3(kThreads), 0, stream, a);
       CP25_LAUNCH_CHECK();
       kern = xk ? attn_fwd_m16<1, true, 2, false, 2> : attn_fwd_m16<0, true, 2, false, 2>;
@@ -1682,8 +1687,8 @@ extern "C" int cp25_attn_fwd_prescaled_qnorm(const void* q, const void* k, const
 extern "C" const char* cp25_attn_kernel(int Lk, float softmax_scale, float q_norm_bound, float k_norm_bound,
                                         int prescaled, int fp8) {
   if (prescaled == 2 && m16_mode(q_norm_bound, k_norm_bound, 1.f, true) != 1)  // cp25_attn_fwd_prescaled_kslots
-    return Lk <= 4096 ? "attn_fwd_m16<cross, prescaled, gated zero shift | online max>"
-                      : "attn_fwd_m16<self, prescaled, gated zero shift | online max>";
+    return Lk <= 4096 ? "attn_fwd_m16<cross, prescaled, gated fixed shift | online max>"
+                      : "attn_fwd_m16<self, prescaled, gated fixed shift | online max>";
   if (fp8 == 2) return Lk <= 4096 ? "attn_fwd_f8<cross, fp8 Q K^T + fp8 P.V>" : "attn_fwd_f8<self, fp8 Q K^T + fp8 P.V>";
   if (fp8 == 1) return Lk <= 4096 ? "attn_fwd_f8<cross, fp8 Q K^T>" : "attn_fwd_f8<self, fp8 Q K^T>";
   if (Lk <= 4096) {

@@ -1,12 +1,12 @@
-"""The gated zero-shift / online-max attention pair (cp25_attn_fwd_prescaled_kslots) and its data-tight key bound
+"""The gated fixed-shift / online-max attention pair (cp25_attn_fwd_prescaled_kslots) and its data-tight key bound
 (cp25_head_rmsnorm_rope_nmax).
 
 Reference op: networks/attention.py:90-181 after the q/k RMSNorms of minimal_v4_dit.py:355-358 (learnable weights:
 a trained checkpoint's max|w| puts the weight-based bound sqrt(128) max|w_q| max|w_k| past the zero-shift window).
 The k RMSNorm kernel measures the max |k row| it writes; with it a 256-query block whose bound max|q_row| max|k|
-is <= 96 runs the zero-shift loop, any other block the online max. Checks: the measured bound equals the true max
-row norm; every block's output is bit-identical to the mode it was routed to (zero shift / online max, each launched
-on its own); attention tolerance vs fp32 (4e-3, tests/test_attention_gpu.py).
+is <= 110 runs the fixed-shift loop on that measured bound (round 6; it was the zero shift up to 96), any other block
+the online max. Checks: the measured bound equals the true max row norm; every block's output is bit-identical to the
+mode it was routed to (fixed shift / online max, each launched on its own); attention tolerance vs fp32 (4e-3, tests/test_attention_gpu.py).
 """
 import pytest
 import torch
@@ -76,28 +76,30 @@ def test_gated_pair_routes_blocks_bit_identically(device, B, H, L, mixed):
     slots = torch.zeros((64, 32), dtype=torch.float32, device=device)
     slots[3, 0] = k.float().norm(dim=-1).max()  # what head_rmsnorm_rope_nmax would write (any slot)
     o = N.attn_fwd(qs, k, v, prescaled=True, norm_bounds=(qb, kb), k_norm_slots=slots, n_split=1)
-    # the two modes on their own: zero shift (bounds that allow it) and online max (no bounds)
-    o_zero = N.attn_fwd(qs, k, v, prescaled=True, norm_bounds=(0.1, 0.1), n_split=1)
+    # the two modes on their own: the fixed shift with the measured key bound x 1.001 (fp32, as the kernel forms it;
+    # a q bound that makes the product 97 selects the fixed mode) and the online max (no bounds)
+    kd = (slots[3:4, 0] * torch.tensor([1.001], dtype=torch.float32, device=device)).item()
+    o_fixed = N.attn_fwd(qs, k, v, prescaled=True, norm_bounds=(97.0 / kd, kd), n_split=1)
     o_onl = N.attn_fwd(qs, k, v, prescaled=True, n_split=1)
     torch.cuda.synchronize()
     kmax = k.float().norm(dim=-1).max().item()
     nblk = (L + 255) // 256
-    n_zero = 0
+    n_fixed = 0
     for b in range(B):
         for h in range(H):
             for j in range(nblk):
                 r = slice(256 * j, min(256 * (j + 1), L))
                 qmax = qs[b, r, h].float().norm(dim=-1).max().item()
-                zero_ok = qmax * kmax * 1.001 <= 96.0
-                n_zero += zero_ok
-                want = o_zero if zero_ok else o_onl
-                assert torch.equal(o[b, r, h], want[b, r, h]), (b, h, j, zero_ok)
+                fixed_ok = qmax * kmax * 1.001 <= 110.0  # attn_common.h kGateFixed
+                n_fixed += fixed_ok
+                want = o_fixed if fixed_ok else o_onl
+                assert torch.equal(o[b, r, h], want[b, r, h]), (b, h, j, fixed_ok)
     e = _rel(o, _ref(qs, k, v, 1.0 / LOG2E))
-    print(f"gated B={B} H={H} L={L} mixed={mixed}: {n_zero}/{B * H * nblk} blocks zero-shift, vs fp32 {e:.2e}")
+    print(f"gated B={B} H={H} L={L} mixed={mixed}: {n_fixed}/{B * H * nblk} blocks fixed-shift, vs fp32 {e:.2e}")
     assert e <= TOL
-    assert n_zero > 0
+    assert n_fixed > 0
     if not mixed:
-        assert n_zero == B * H * nblk
+        assert n_fixed == B * H * nblk
     assert torch.isfinite(o.float()).all()
 
 

@@ -16,10 +16,11 @@ match the single-rank run (guidance 0, 2 Karras steps = 3 evals x CFG).
   fp8 attention too (q / k scales are fixed powers of two, V's per-head scale is taken over the gathered
   keys, which every rank holds whole).
 * trained-size q/k norm weights (uniform in [0.5, 3], bound product ~147): CP > 1 runs the online-max attention on the
-  weight bounds, and so does CP = 1 by default (round 4): bit-identity ("nw_weight", under CP25_ATTN_SPLIT=1 like
+  weight bounds, and so does CP = 1 with data_tight_k_bound off: bit-identity ("nw_weight", under CP25_ATTN_SPLIT=1 like
   every bit-exact case here: the default tail split runs the blocks of a launch's last partial round as key-range
-  splits, and which blocks those are depends on the launch's workgroup count mod the CU count). The opt-in gated pair at CP = 1
-  (data_tight_k_bound = True: zero shift for every 256-query block whose measured bound allows it, chosen per block of
+  splits, and which blocks those are depends on the launch's workgroup count mod the CU count). The gated pair at CP = 1
+  (data_tight_k_bound = True, the default since round 6: the fixed shift on the measured key bound for every 256-query
+  block it allows, chosen per block of
   the whole sequence, the max |k| taken over the whole CFG batch) rounds P at other shifts: against it the distance is
   rounding ("nw_gated", <= 1.5e-2 like the split plan's).
 """
@@ -121,8 +122,8 @@ def test_cp2_matches_cp1(device, monkeypatch, world, split_env, tol, precision):
     m.net.force_lanes = bool(split_env)
     if precision.startswith("nw_"):
         kern = m.net.attention_kernels(shape[1] * shape[2] * shape[3] // 4)
-        assert "online" in kern["self"], kern  # CP = 1's default with these weights: the CP path's own mode
-        m.net.data_tight_k_bound = precision == "nw_gated"  # opt-in gated pair at CP = 1
+        assert "online" in kern["self"], kern  # the online max (CP = 1: inside the default gated pair; the CP path's mode)
+        m.net.data_tight_k_bound = precision == "nw_gated"  # the gated pair at CP = 1 (default), or the online max
     ref = _run(m, gt, cc, cu, shape, device)
     del m
     torch.cuda.empty_cache()

@@ -4,7 +4,9 @@ shift (forced by inflating every block's q bound so the product lands at 80, ins
 by evaluation in one process, in ABBA order so that clock drift over the run cancels. The bench.py workload
 (Predict2.5-2B Image2World 704x1280x121f, CFG 2, B = 2, L = 109 120, unit norm weights).
 
-  python tools/ab_whole_shift.py [--pairs 6]
+  python tools/ab_whole_shift.py [--pairs 6] [--trained]
+--trained: q/k norm weights uniform in [0.5, 3] (bound product ~147: the online max) and the A/B is the gated pair
+(net.data_tight_k_bound: blocks whose measured bound is <= 110 run the fixed shift on it) against the online max.
 Prints one JSON line: ms per evaluation for each form (list and median), their ratio and the kernel names.
 """
 import argparse
@@ -22,6 +24,7 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pairs", type=int, default=6)
+    ap.add_argument("--trained", action="store_true")
     a = ap.parse_args()
     from cosmos_predict2 import _native as N
     from cosmos_predict2.pipeline import DEFAULT_NEGATIVE_PROMPT, Video2WorldInference
@@ -33,6 +36,12 @@ def main():
     model = pipe.model
     net = model.net
     L = state_t * (h // 16) * (w // 16)
+    if a.trained:
+        gw = torch.Generator(device=dev).manual_seed(7)
+        for k_, w_ in net.sd.items():
+            if k_.endswith(("q_norm.weight", "k_norm.weight")):
+                w_.copy_((0.5 + 2.5 * torch.rand(w_.shape, device=dev, generator=gw)).to(w_.dtype))
+        net.refresh_norm_bounds()
     whole = list(net.attn_bounds)
     c = 128 ** -0.5 * 1.4426950408889634
     zero = [(80.0 / (c * kb), kb) if qb * c * kb < 80.0 else (qb, kb) for qb, kb in whole]
@@ -51,7 +60,10 @@ def main():
                                    num_conditional_frames=1, guidance=7, seed=0, num_steps=35)
 
         def one(form):
-            net.attn_bounds = whole if form == "whole" else zero
+            if a.trained:  # "whole": the gated pair (fixed shift on the measured key bound), "zero": the online max
+                net.data_tight_k_bound = form == "whole"
+            else:
+                net.attn_bounds = whole if form == "whole" else zero
             names[form] = net.attention_kernels(L)["self"]
             if run.done:
                 run.restart()
@@ -70,9 +82,10 @@ def main():
             for f in order:
                 t[f].append(round(one(f), 2))
         net.attn_bounds = whole
+        net.data_tight_k_bound = False
     med = {f: float(np.median(v)) for f, v in t.items()}
     print(json.dumps({"ms_per_eval": t, "median": med, "whole_over_zero": med["whole"] / med["zero"],
-                      "kernels": names}))
+                      "kernels": names, "trained_norm_weights": a.trained}))
 
 
 if __name__ == "__main__":
