@@ -1354,15 +1354,23 @@ int plan_split(int B, int H, int Lq, int Lk) {
 
 // The m16 softmax-shift mode for these bounds (the bound product in log2 units; |q_row| <= q_norm_bound): 1 zero
 // shift (pre-scaled q, product <= 96), 0 fixed per-row shift (product <= 98), 2 online max (larger or unknown).
-// whole_ok (long-key self-attention launches, round 6): a product <= kWhole takes the fixed mode, whose rows then
-// shift by their whole bound (P <= 2): measured 0.8 % faster than the zero shift at the metric launch, the same cycles
-// at a higher power-limited clock (profiles/r6/shift_power/). Short-key launches keep the zero shift (the persistent
-// cross-attention has no fixed mode).
+// whole_ok (long-key self-attention launches, round 6): a product <= kGateFixed (110) takes the fixed mode, whose rows
+// then shift by their whole bound to b_row 63 (P <= 2) and by floor(126 - b_row) past it (P <= 2^95): small P, measured
+// 0.8 % faster than the zero shift at the metric launch, the same cycles at a higher power-limited clock
+// (profiles/r6/shift_power/). Short-key launches keep the zero shift (the persistent cross-attention has no fixed mode).
 int m16_mode(float q_norm_bound, float k_norm_bound, float scale_log2, bool prescaled, bool whole_ok = false) {
   const double bb = (double)q_norm_bound * k_norm_bound * (prescaled ? 1.0 : scale_log2);
-  if (!(q_norm_bound > 0.f && k_norm_bound > 0.f) || bb > kMaxBound) return 2;
-  if (whole_ok && bb <= kWhole) return 0;
+  if (!(q_norm_bound > 0.f && k_norm_bound > 0.f)) return 2;
+  if (whole_ok && bb <= kGateFixed) return 0;
+  if (bb > kMaxBound) return 2;
   return prescaled && bb <= kTop ? 1 : 0;
+}
+
+// The gated pair (k-norm slots given) runs where the weight bounds alone would leave the launch on the online max
+// (long keys: past kGateFixed; short keys: past the zero-shift window)
+bool m16_gated(float q_norm_bound, float k_norm_bound, bool long_keys) {
+  return long_keys ? m16_mode(q_norm_bound, k_norm_bound, 1.f, true, true) == 2
+                   : m16_mode(q_norm_bound, k_norm_bound, 1.f, true) != 1;
 }
 
 // Short-key (text cross-attention) launches: 1 = the persistent form (attn_fwd_m16<.., kPersist>), 0 = one workgroup
@@ -1511,7 +1519,7 @@ static int attn_launch(const void* q, const void* k, const void* v, void* o, int
     void (*kern_tail)(AttnArgs) = nullptr;  // the tail segments' symbol (plan_tail: self-attention shapes only)
     int64_t grid = nwg;
     int threads = kThreads;
-    if (prescaled && kslots && m16_mode(q_norm_bound, k_norm_bound, 1.f, true) != 1) {
+    if (prescaled && kslots && m16_gated(q_norm_bound, k_norm_bound, !xk)) {
       // the gated pair: blocks whose data-tight bound allows it (<= kGateFixed) run the fixed-shift loop with the
       // measured key bound, the others the online max
       hipLaunchKernelGGL((xk ? attn_fwd_m16<1, true, 0, false, 1> : attn_fwd_m16<0, true, 0, false, 1>),
@@ -1686,7 +1694,7 @@ extern "C" int cp25_attn_fwd_prescaled_qnorm(const void* q, const void* k, const
 
 extern "C" const char* cp25_attn_kernel(int Lk, float softmax_scale, float q_norm_bound, float k_norm_bound,
                                         int prescaled, int fp8) {
-  if (prescaled == 2 && m16_mode(q_norm_bound, k_norm_bound, 1.f, true) != 1)  // cp25_attn_fwd_prescaled_kslots
+  if (prescaled == 2 && m16_gated(q_norm_bound, k_norm_bound, Lk > 4096))  // cp25_attn_fwd_prescaled_kslots
     return Lk <= 4096 ? "attn_fwd_m16<cross, prescaled, gated fixed shift | online max>"
                       : "attn_fwd_m16<self, prescaled, gated fixed shift | online max>";
   if (fp8 == 2) return Lk <= 4096 ? "attn_fwd_f8<cross, fp8 Q K^T + fp8 P.V>" : "attn_fwd_f8<self, fp8 Q K^T + fp8 P.V>";

@@ -115,6 +115,9 @@ def test_gated_pair_without_slots_is_online(device):
 
 def test_gated_kernel_name(device):
     assert "gated" in N.attn_kernel_name(109120, norm_bounds=(4.4, 34.6), prescaled=2)
-    # inside the zero-shift window no gate: a long-key launch with a product <= 63 takes the whole-bound fixed shift
+    # no gate where the weight bounds suffice: long keys take the fixed shift up to a product of 110 (whole bound to 63),
+    # short keys the zero shift up to 96
     assert "fixed shift" in N.attn_kernel_name(109120, norm_bounds=(1.5, 11.6), prescaled=2)
-    assert "zero shift" in N.attn_kernel_name(109120, norm_bounds=(7.0, 11.6), prescaled=2)
+    assert "fixed shift" in N.attn_kernel_name(109120, norm_bounds=(8.5, 12.5), prescaled=2)
+    assert "gated" in N.attn_kernel_name(109120, norm_bounds=(9.0, 12.5), prescaled=2)
+    assert "zero shift" in N.attn_kernel_name(512, norm_bounds=(7.0, 11.6), prescaled=2)

@@ -70,7 +70,7 @@ def test_m16_modes_match_fp32(device, B, H, Lq, Lk, n_split, prescaled):
         assert qb * kn <= 63.0
         exp = "fixed shift" if Lk > 4096 else "zero shift"
         assert exp in N.attn_kernel_name(Lk, norm_bounds=(qb, kn), prescaled=True)
-        assert "zero shift" in N.attn_kernel_name(Lk, norm_bounds=(max(qb, 80.0 / kn), kn), prescaled=True)
+        assert exp in N.attn_kernel_name(Lk, norm_bounds=(max(qb, 80.0 / kn), kn), prescaled=True)  # to 110 / 96
     else:
         qin = q
         ref = ref_attention(q, k, v, scale)
@@ -206,20 +206,24 @@ def test_m16_full_metric_shape_query_slice(device):
         del o, oc, qs, k, v
 
 
-def test_m16_zero_shift_top_of_window_long_keys(device):
-    """The zero-shift window's headroom (attn_fwd.hip kTop = 96): every score of every row at the top of the window
-    (q and k aligned, 95.9 log2 units) over 163 840 keys (> config 4's 163 800), |v| up to ~400: the row sum reaches
-    2^113.2 and O ~2^122, inside fp32 (the window holds while |v| Lk < 2^32). All terms equal, so O = mean(v) exactly
-    up to the bf16 output rounding."""
-    Lq, Lk = 256, 163840
+@pytest.mark.parametrize("Lk,k0,kb,form", [(163840, 11.984375, 12.0, "fixed shift"), (163840, 13.75, 13.75, "fixed shift"),
+                                            (4096, 11.984375, 12.0, "zero shift")])
+def test_m16_zero_shift_top_of_window_long_keys(device, Lk, k0, kb, form):
+    """The windows' headroom: every score of every row at the top of the window over 163 840 keys (> config 4's
+    163 800), |v| up to ~400. Long keys take the fixed shift (round 6) up to a bound product of 110 (attn_common.h
+    kGateFixed): scores 95.9 and 110 are shifted by floor(126 - b_row) = 30 / 16, so P = 2^65.9 / 2^94 and O stays inside
+    fp32; the zero shift (attn_fwd.hip kTop = 96, short keys here) leaves P = 2^95.9 (the row sum 2^107, O ~2^116 over
+    4096 keys; the window holds while |v| Lk < 2^32). All terms equal, so O = mean(v) exactly up to the bf16 output
+    rounding."""
+    Lq = 256
     g = torch.Generator(device="cpu").manual_seed(13)
     q = torch.zeros(1, Lq, 1, 128)
     k = torch.zeros(1, Lk, 1, 128)
-    q[..., 0], k[..., 0] = 8.0, 11.984375  # bf16-exact; pre-scaled score 95.875 (log2 units)
+    q[..., 0], k[..., 0] = 8.0, k0  # bf16-exact; pre-scaled score 95.875 / 110 (log2 units)
     v = (torch.randn(1, Lk, 1, 128, generator=g) * 100.0).to(device, torch.bfloat16)
     q, k = q.to(device, torch.bfloat16), k.to(device, torch.bfloat16)
-    assert N.attn_kernel_name(Lk, None, (8.0, 12.0), True).endswith("zero shift>")
-    o = N.attn_fwd(q, k, v, norm_bounds=(8.0, 12.0), prescaled=True)
+    assert form in N.attn_kernel_name(Lk, None, (8.0, kb), True)
+    o = N.attn_fwd(q, k, v, norm_bounds=(8.0, kb), prescaled=True)
     torch.cuda.synchronize()
     assert torch.isfinite(o.float()).all()
     mean_v = v.float().mean(1)[0, 0]
