@@ -21,10 +21,10 @@ constexpr int kThreads = kWaves * 64;
 // contract guard below poisons a row whose sum overflows. bf16 P has the fp32 exponent range.
 constexpr float kTop = 96.f;        // zero / fixed shift: largest exponent a term may reach
 constexpr float kMaxBound = 98.f;   // fixed shift: largest score bound b (smallest row-max term 2^(96 - 2 b) >= 2^-100)
-constexpr float kWhole = 63.f;      // fixed shift, whole-bound form: a row with b_row <= 63 is shifted by floor(b_row), so
-                                    // P <= 2 and its largest term >= 2^(-2 b_row) >= 2^-126 (round 6: small P runs the
-                                    // power-limited loop faster, tools/lab/ab_shift_power.py); a row past 63 by
-                                    // floor(126 - b_row): P <= 2^(2 b_row - 125), its largest term still >= 2^-126
+constexpr float kPDrop = 60.f;      // fixed shift (round 6): rows shift by floor(min(b_row + 60, 126 - b_row)), so
+                                    // P <= 2^-59 where b_row <= 33 and P <= 2^(2 b_row - 125) past it, the row's
+                                    // largest term >= 2^-126. Small P runs the power-limited loop faster (P <= 2 vs
+                                    // 2^17: -0.8 %; 2^-59 vs 2: -0.7 %, profiles/r6/shift_power/)
 constexpr float kGateFixed = 110.f; // gated pair: a block whose data-tight bound is <= 110 runs the fixed shift, whose
                                     // rows then keep P <= 2^(2 * 110 - 125) = 2^95 (inside the zero-shift window's 2^96)
 constexpr float kTopF8 = 60.f;      // fp8 Q K^T form: P = exp2(S) unshifted for bound products up to this

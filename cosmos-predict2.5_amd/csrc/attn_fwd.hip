@@ -10,8 +10,8 @@
 //                 K/V 64-key tiles double-buffered in padded LDS rows, counted-lgkmcnt operand ring, row sums by
 //                 MFMA, XCD-aware grid. The softmax shift of a query row enters as the initial C of its Q K^T MFMA
 //                 chains, so P = exp2(S) needs no per-score VALU beyond the exp (prescaled q). The shift is either
-//                 fixed from a norm bound (b_row = |q_row| max|k| <= 98: shift floor(b_row) where b_row <= 63, else
-//                 max(b_row - 96, 0); no max at all) or
+//                 fixed from a norm bound (b_row = |q_row| max|k|: shift floor(min(b_row + 60, 126 - b_row)), small
+//                 P, no max at all) or
 //                 an online row max with lazy rescale (any data; per wave, decided at the kernel start).
 //   attn_fwd_f8   the config-5 fp8 option (no reference counterpart): Q K^T on v_mfma_f32_32x32x64_f8f6f4 over e4m3
 //                 q / k, and with kF8 = 3 also P.V on e5m2 P (made without exp2) and e4m3 V^T tiles.
@@ -52,9 +52,9 @@ using namespace cp25attn;
 // the fp32 / bf16 range. With a pre-scaled q (rows carry softmax_scale * log2 e) the shift is the initial C of the
 // row's Q K^T chains, so S arrives already shifted:
 //   zero   (pre-scaled q, bound product b <= 96): no shift; terms in [2^-b, 2^b];
-//   fixed  (b <= 98): from the row's own |q_row|: shift floor(b_row) if b_row <= 63 (the whole bound: P <= 2, the
-//          row's largest term >= 2^-126; the host's choice for self-attention with b <= 63, round 6), else
-//          max(b_row - 96, 0) (the row's largest term >= 2^-100);
+//   fixed  (b <= 98; long keys b <= 110, round 6): from the row's own |q_row|: shift floor(min(b_row + 60,
+//          126 - b_row)): P <= 2^-59 where b_row <= 33, P <= 2^(2 b_row - 125) past it, the row's largest term
+//          >= 2^-126 (kPDrop in attn_common.h);
 //   online (larger or unknown bounds): tile 0 sets the shift to the row max; a later tile rescales O and the row sum
 //          (and moves the shift) only for a row whose max exceeds the shift by more than kLazy (24), so P <= 2^24 and
 //          the row's largest term >= 1. Per tile: 16 v_max3 per lane and one ballot; the row reduction (two row swaps)
@@ -427,10 +427,11 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_m16(AttnArgs a) {
           const float x = static_cast<float>(qf[qh][s][e]);
           qq = fmaf(x, x, qq);
         }
-      // b_row = |q_row| max|k| bounds every score of the row (log2 units). Whole-bound form (b_row <= kWhole): shift
-      // floor(b_row), P <= 2; past it floor(126 - b_row) (P <= 2^(2 b_row - 125), the largest term >= 2^-126)
+      // b_row = |q_row| max|k| bounds every score of the row (log2 units). Shift floor(min(b_row + kPDrop, 126 - b_row)):
+      // P <= 2^(1 - kPDrop) = 2^-59 where b_row <= 33, else P <= 2^(2 b_row - 125); the row's largest term >= 2^-126
+      // (its scores are >= -b_row). Small P costs the power-limited loop less energy (profiles/r6/shift_power/).
       const float b_row = sqrtf(group4_sum(qq)) * gate_kbound * cs;
-      m_run[qh] = floorf(b_row <= kWhole ? b_row : 126.f - b_row);
+      m_run[qh] = floorf(fminf(b_row + kPDrop, 126.f - b_row));
     }
   }
   f32x4 minit[2];  // kPre: -shift, the Q K^T chains' initial C

@@ -231,20 +231,21 @@ def test_m16_zero_shift_top_of_window_long_keys(device, Lk, k0, kb, form):
 
 
 @pytest.mark.parametrize("sign", [1.0, -1.0])
-def test_m16_whole_bound_shift_edges(device, sign):
-    """The whole-bound fixed shift (round 6: long-key launches whose bound product is <= kWhole = 63 shift each row by
-    floor(b_row)): every score at +b (the top, P = 2^(b - floor(b)) <= 2) or at -b (the bottom: P = 2^(-2 b + ...) at
-    b = 62.5, down to 2^-125, still a normal bf16 / fp32), over 8192 keys. All terms equal, so O = mean(v) up to the
-    bf16 output rounding."""
+@pytest.mark.parametrize("k0", [12.5, 3.40625])
+def test_m16_whole_bound_shift_edges(device, sign, k0):
+    """The fixed shift of long-key launches (round 6: each row shifted by floor(min(b_row + 60, 126 - b_row)),
+    attn_common.h kPDrop): every score at +b (the top) or at -b (the bottom) over 8192 keys. b = 62.5: shift 63, P =
+    2^-0.5 / 2^-125.5 (still a normal bf16 / fp32); b = 17.03 (the unit weights' range): shift 77, P = 2^-60 / 2^-94.
+    All terms equal, so O = mean(v) up to the bf16 output rounding."""
     Lq, Lk = 256, 8192
     g = torch.Generator(device="cpu").manual_seed(14)
     q = torch.zeros(1, Lq, 1, 128)
     k = torch.zeros(1, Lk, 1, 128)
-    q[..., 0], k[..., 0] = 5.0, sign * 12.5  # bf16-exact; pre-scaled score +-62.5 (log2 units)
+    q[..., 0], k[..., 0] = 5.0, sign * k0  # bf16-exact; pre-scaled score +-62.5 / +-17.03 (log2 units)
     v = (torch.randn(1, Lk, 1, 128, generator=g) * 10.0).to(device, torch.bfloat16)
     q, k = q.to(device, torch.bfloat16), k.to(device, torch.bfloat16)
-    assert N.attn_kernel_name(Lk, None, (5.0, 12.5), True).endswith("fixed shift>")
-    o = N.attn_fwd(q, k, v, norm_bounds=(5.0, 12.5), prescaled=True)
+    assert N.attn_kernel_name(Lk, None, (5.0, k0), True).endswith("fixed shift>")
+    o = N.attn_fwd(q, k, v, norm_bounds=(5.0, k0), prescaled=True)
     torch.cuda.synchronize()
     assert torch.isfinite(o.float()).all()
     mean_v = v.float().mean(1)[0, 0]

@@ -1,4 +1,7 @@
-"""A/B of the self-attention's softmax-shift form inside the metric's sampler evaluation (round 6): the whole-bound
+"""(Written before long-key launches took the fixed shift up to a bound product of 110: since then the inflated q bound
+below no longer selects the zero shift, so the unit-weight A/B compares the fixed shift with itself; the --trained
+A/B is unaffected. Results: profiles/r6/shift_power/.)
+A/B of the self-attention's softmax-shift form inside the metric's sampler evaluation (round 6): the whole-bound
 fixed shift (the default for bound products <= 63: each row shifted by floor(|q_row| max|k|), P <= 2) vs the zero
 shift (forced by inflating every block's q bound so the product lands at 80, inside the zero-shift window), evaluation
 by evaluation in one process, in ABBA order so that clock drift over the run cancels. The bench.py workload

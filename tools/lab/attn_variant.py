@@ -126,6 +126,13 @@ PATCHES = {
     # shift loop (P scaled by an exact power of two). Lab probe of whether P's magnitude moves the power-limited clock
     "dshift": [("      m_run[qh] = fmaxf(sqrtf(group4_sum(qq)) * a.kbound * cs - kTop, 0.f);\n",
                 "      m_run[qh] = floorf(sqrtf(group4_sum(qq)) * a.kbound * cs);\n")],
+    # round 6: the whole-bound shift pushed further down (rows with b_row <= 30 shift by floor(b_row) + 24 / + 60: P <=
+    # 2^-23 / 2^-59): does an even smaller P save more energy? (unit-weight data: b_row ~17). These two and `dshift`
+    # patch attn_fwd.hip as it was before the product took the result (kPDrop): build them from that commit's source
+    "shift_p24": [("      m_run[qh] = floorf(b_row <= kWhole ? b_row : 126.f - b_row);\n",
+                   "      m_run[qh] = floorf(b_row <= 30.f ? b_row + 24.f : (b_row <= kWhole ? b_row : 126.f - b_row));\n")],
+    "shift_p60": [("      m_run[qh] = floorf(b_row <= kWhole ? b_row : 126.f - b_row);\n",
+                   "      m_run[qh] = floorf(b_row <= 30.f ? b_row + 60.f : (b_row <= kWhole ? b_row : 126.f - b_row));\n")],
     "none": [],
 }
 
